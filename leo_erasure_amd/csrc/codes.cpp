@@ -1,0 +1,284 @@
+// codes.cpp — see codes.hpp.  Host-side construction of the code matrices;
+// the GPU kernels only ever see the resulting coefficient / bit tables.
+#include "codes.hpp"
+
+#include <algorithm>
+#include <array>
+#include <memory>
+#include <mutex>
+
+#include "../../include/leoec.h"
+
+namespace leoec {
+
+namespace {
+
+// gf-complete / Jerasure default primitive polynomials, indexed by w (octal,
+// as in the published tables).  w = 32 carries its x^32 term implicitly.
+constexpr uint64_t kDefaultPoly[33] = {
+    0,         01,         07,         013,         023,        045,
+    0103,      0211,       0435,       01021,       02011,      04005,
+    010123,    020033,     042103,     0100003,     0210013,    0400011,
+    01000201,  02000047,   04000011,   010000005,   020000003,  040000041,
+    0100000207, 0200000011, 0400000107, 01000000047, 02000000011, 04000000005,
+    010040000007, 020000000011, 00020000007};
+
+}  // namespace
+
+Field::Field(int w) : w_(w) {
+  poly_ = (w == 32) ? ((1ull << 32) | kDefaultPoly[32]) : kDefaultPoly[w];
+  if (w >= 2 && w <= 16) {
+    // the default polynomials are primitive: x = 2 generates the group
+    const uint32_t n = (1u << w) - 1;
+    log_.assign(n + 1, 0);
+    exp_.assign(2 * n, 0);
+    uint32_t v = 1;
+    for (uint32_t i = 0; i < n; ++i) {
+      exp_[i] = exp_[i + n] = v;
+      log_[v] = i;
+      v = slow_mul(v, 2);
+    }
+  }
+}
+
+uint32_t Field::slow_mul(uint32_t a, uint32_t b) const {
+  if (w_ == 1) return a & b & 1u;
+  uint64_t acc = 0;
+  for (uint64_t x = a; b; b >>= 1, x <<= 1)
+    if (b & 1) acc ^= x;
+  for (int bit = 2 * w_ - 2; bit >= w_; --bit)
+    if ((acc >> bit) & 1) acc ^= poly_ << (bit - w_);
+  return (uint32_t)acc;
+}
+
+uint32_t Field::mul(uint32_t a, uint32_t b) const {
+  if (a == 0 || b == 0) return 0;
+  if (!log_.empty()) return exp_[log_[a] + log_[b]];
+  return slow_mul(a, b);
+}
+
+uint32_t Field::inv(uint32_t a) const {
+  if (a == 0) return 0;
+  if (!log_.empty()) {
+    const uint32_t n = (1u << w_) - 1;
+    return exp_[(n - log_[a]) % n];
+  }
+  // a^(2^w - 2) by square-and-multiply
+  uint64_t e = (w_ == 32) ? 0xFFFFFFFEull : ((1ull << w_) - 2);
+  uint32_t r = 1;
+  for (uint32_t sq = a; e; e >>= 1, sq = mul(sq, sq))
+    if (e & 1) r = mul(r, sq);
+  return r;
+}
+
+int Field::bit_weight(uint32_t a) const {
+  int ones = 0;
+  for (int x = 0; x < w_; ++x, a = mul(a, 2)) ones += __builtin_popcount(a);
+  return ones;
+}
+
+const Field& field(int w) {
+  static std::array<std::unique_ptr<Field>, 33> fields;
+  static std::array<std::once_flag, 33> once;
+  std::call_once(once[w], [w] { fields[w].reset(new Field(w)); });
+  return *fields[w];
+}
+
+// ---------------------------------------------------------------------------
+// vandrs: systematic form of the extended Vandermonde matrix, coding row 0 and
+// column 0 normalised to ones (Jerasure reed_sol_big_vandermonde_distribution_matrix).
+int vandermonde_coding_matrix(int k, int m, int w, GfMatrix* out) {
+  const int rows = k + m, cols = k;
+  if (w < 30 && ((1ll << w) < rows)) return LEOEC_E_UNSUPPORTED;
+  const Field& F = field(w);
+  GfMatrix V;
+  V.rows = rows; V.cols = cols; V.a.assign((size_t)rows * cols, 0);
+  V.at(0, 0) = 1;
+  V.at(rows - 1, cols - 1) = 1;
+  for (int r = 1; r + 1 < rows; ++r) {
+    uint32_t p = 1;
+    for (int c = 0; c < cols; ++c, p = F.mul(p, (uint32_t)r)) V.at(r, c) = p;
+  }
+  // column operations bring the top k x k block to the identity
+  for (int i = 1; i < cols; ++i) {
+    int piv = i;
+    while (piv < rows && V.at(piv, i) == 0) ++piv;
+    if (piv == rows) return LEOEC_E_UNSUPPORTED;
+    if (piv != i)
+      for (int c = 0; c < cols; ++c) std::swap(V.at(i, c), V.at(piv, c));
+    if (V.at(i, i) != 1) {
+      const uint32_t s = F.inv(V.at(i, i));
+      for (int r = 0; r < rows; ++r) V.at(r, i) = F.mul(s, V.at(r, i));
+    }
+    for (int c = 0; c < cols; ++c) {
+      const uint32_t e = V.at(i, c);
+      if (c == i || e == 0) continue;
+      for (int r = 0; r < rows; ++r) V.at(r, c) ^= F.mul(e, V.at(r, i));
+    }
+  }
+  for (int c = 0; c < cols; ++c) {  // first coding row -> ones
+    const uint32_t t = V.at(cols, c);
+    if (t == 1) continue;
+    const uint32_t s = F.inv(t);
+    for (int r = cols; r < rows; ++r) V.at(r, c) = F.mul(s, V.at(r, c));
+  }
+  for (int r = cols + 1; r < rows; ++r) {  // first column -> ones
+    const uint32_t t = V.at(r, 0);
+    if (t == 1) continue;
+    const uint32_t s = F.inv(t);
+    for (int c = 0; c < cols; ++c) V.at(r, c) = F.mul(V.at(r, c), s);
+  }
+  out->rows = m; out->cols = k;
+  out->a.assign(V.a.begin() + (size_t)k * k, V.a.end());
+  return LEOEC_OK;
+}
+
+// cauchyrs: Jerasure cauchy_good_general_coding_matrix.  For m = 2 the
+// second row is the published "cbest" list: nonzero elements ordered by the
+// weight of their bitmatrix (ties by value); otherwise cauchy_original
+// (1 / (i xor (m + j))) followed by cauchy_improve_coding_matrix.
+int cauchy_good_coding_matrix(int k, int m, int w, GfMatrix* out) {
+  const Field& F = field(w);
+  out->rows = m; out->cols = k; out->a.assign((size_t)m * k, 0);
+  const long cbest_limit = w < 2 ? -1 : (w <= 11 ? (1l << w) - 1 : 1023);
+  if (m == 2 && k <= cbest_limit) {
+    if (w > 20) return LEOEC_E_UNSUPPORTED;
+    std::vector<std::pair<int, uint32_t>> order;
+    const uint32_t n = (1u << w) - 1;
+    order.reserve(n);
+    for (uint32_t e = 1; e <= n; ++e) order.emplace_back(F.bit_weight(e), e);
+    std::partial_sort(order.begin(), order.begin() + k, order.end());
+    for (int j = 0; j < k; ++j) { out->at(0, j) = 1; out->at(1, j) = order[j].second; }
+    return LEOEC_OK;
+  }
+  if (w < 31 && (long long)(k + m) > (1ll << w)) return LEOEC_E_UNSUPPORTED;
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < k; ++j) out->at(i, j) = F.inv((uint32_t)(i ^ (m + j)));
+  // improve: columns scaled so row 0 is all ones ...
+  for (int j = 0; j < k; ++j) {
+    const uint32_t t = out->at(0, j);
+    if (t == 1) continue;
+    const uint32_t s = F.inv(t);
+    for (int i = 0; i < m; ++i) out->at(i, j) = F.mul(out->at(i, j), s);
+  }
+  // ... then each later row divided by the element that minimises its weight
+  for (int i = 1; i < m; ++i) {
+    int best = 0;
+    for (int j = 0; j < k; ++j) best += F.bit_weight(out->at(i, j));
+    int pick = -1;
+    for (int j = 0; j < k; ++j) {
+      if (out->at(i, j) == 1) continue;
+      const uint32_t s = F.inv(out->at(i, j));
+      int weight = 0;
+      for (int x = 0; x < k; ++x) weight += F.bit_weight(F.mul(out->at(i, x), s));
+      if (weight < best) { best = weight; pick = j; }
+    }
+    if (pick >= 0) {
+      const uint32_t s = F.inv(out->at(i, pick));
+      for (int j = 0; j < k; ++j) out->at(i, j) = F.mul(out->at(i, j), s);
+    }
+  }
+  return LEOEC_OK;
+}
+
+// isars: ISA-L gf_gen_cauchy1_matrix, coding rows only: entry (i, j) = 1/(i ^ j)
+// for i = k..k+m-1 (byte arithmetic, GF(2^8)).
+int isal_cauchy1_coding_matrix(int k, int m, GfMatrix* out) {
+  const Field& F = field(8);
+  out->rows = m; out->cols = k; out->a.assign((size_t)m * k, 0);
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < k; ++j) out->at(i, j) = F.inv((uint32_t)(((k + i) ^ j) & 0xFF));
+  return LEOEC_OK;
+}
+
+// liberation: P rows are identity blocks; Q block j has ones at (i, (j+i) mod w)
+// plus, for j > 0, one extra at row y = j(w-1)/2 mod w, column (y+j-1) mod w.
+int liberation_coding_bitmatrix(int k, int w, BitMatrix* out) {
+  if (k > w) return LEOEC_E_UNSUPPORTED;
+  out->resize(2 * w, k * w);
+  for (int j = 0; j < k; ++j) {
+    for (int i = 0; i < w; ++i) {
+      out->set(i, j * w + i, true);
+      out->set(w + i, j * w + (j + i) % w, true);
+    }
+    if (j > 0) {
+      const int y = (j * ((w - 1) / 2)) % w;
+      out->set(w + y, j * w + (y + j - 1) % w, true);
+    }
+  }
+  return LEOEC_OK;
+}
+
+// Block (i, j) of the bitmatrix: column x holds the bits of M[i][j] * 2^x.
+void expand_to_bitmatrix(const GfMatrix& m, int w, BitMatrix* out) {
+  const Field& F = field(w);
+  out->resize(m.rows * w, m.cols * w);
+  for (int i = 0; i < m.rows; ++i)
+    for (int j = 0; j < m.cols; ++j) {
+      uint32_t e = m.at(i, j);
+      for (int x = 0; x < w; ++x, e = F.mul(e, 2))
+        for (int l = 0; l < w; ++l)
+          if ((e >> l) & 1) out->set(i * w + l, j * w + x, true);
+    }
+}
+
+int gf_invert(const GfMatrix& in, int w, GfMatrix* out) {
+  const Field& F = field(w);
+  const int n = in.rows;
+  GfMatrix a = in;
+  out->rows = out->cols = n;
+  out->a.assign((size_t)n * n, 0);
+  for (int i = 0; i < n; ++i) out->at(i, i) = 1;
+  for (int col = 0; col < n; ++col) {
+    int piv = col;
+    while (piv < n && a.at(piv, col) == 0) ++piv;
+    if (piv == n) return LEOEC_E_NON_INVERTIBLE;
+    if (piv != col)
+      for (int c = 0; c < n; ++c) {
+        std::swap(a.at(col, c), a.at(piv, c));
+        std::swap(out->at(col, c), out->at(piv, c));
+      }
+    const uint32_t s = F.inv(a.at(col, col));
+    for (int c = 0; c < n; ++c) {
+      a.at(col, c) = F.mul(a.at(col, c), s);
+      out->at(col, c) = F.mul(out->at(col, c), s);
+    }
+    for (int r = 0; r < n; ++r) {
+      const uint32_t f = a.at(r, col);
+      if (r == col || f == 0) continue;
+      for (int c = 0; c < n; ++c) {
+        a.at(r, c) ^= F.mul(f, a.at(col, c));
+        out->at(r, c) ^= F.mul(f, out->at(col, c));
+      }
+    }
+  }
+  return LEOEC_OK;
+}
+
+int bit_invert(const BitMatrix& in, BitMatrix* out) {
+  const int n = in.rows;
+  BitMatrix a = in;
+  out->resize(n, n);
+  for (int i = 0; i < n; ++i) out->set(i, i, true);
+  const int W = a.words;
+  for (int col = 0; col < n; ++col) {
+    int piv = col;
+    while (piv < n && !a.get(piv, col)) ++piv;
+    if (piv == n) return LEOEC_E_NON_INVERTIBLE;
+    if (piv != col)
+      for (int x = 0; x < W; ++x) {
+        std::swap(a.row(col)[x], a.row(piv)[x]);
+        std::swap(out->row(col)[x], out->row(piv)[x]);
+      }
+    for (int r = 0; r < n; ++r) {
+      if (r == col || !a.get(r, col)) continue;
+      for (int x = 0; x < W; ++x) {
+        a.row(r)[x] ^= a.row(col)[x];
+        out->row(r)[x] ^= out->row(col)[x];
+      }
+    }
+  }
+  return LEOEC_OK;
+}
+
+}  // namespace leoec

@@ -1,0 +1,578 @@
+// engine.cpp — host side of the engine (see engine.hpp).
+//
+// What runs where: parameter checks, stripe geometry, survivor selection and
+// the k x k (or kw x kw) matrix inversions run on the host, as in the
+// reference; every byte of block data is transformed on the GPU by the
+// kernels of kernels_impl.hpp.  There is no CPU fallback for the data path.
+#include "engine.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <tuple>
+
+#include "../../include/leoec.h"
+
+namespace leoec {
+
+namespace {
+
+bool is_prime_ref(int w) {  // c_src/common.cpp:36-47
+  static const int small[] = {2,   3,   5,   7,   11,  13,  17,  19,  23,  29,  31,  37,  41,  43,
+                              47,  53,  59,  61,  67,  71,  73,  79,  83,  89,  97,  101, 103, 107,
+                              109, 113, 127, 131, 137, 139, 149, 151, 157, 163, 167, 173, 179, 181,
+                              191, 193, 197, 199, 211, 223, 227, 229, 233, 239, 241, 251, 257};
+  for (int p : small)
+    if (w % p == 0) return w == p;
+  return true;
+}
+
+uint64_t round_to(uint64_t n, uint64_t mult) {  // c_src/common.cpp:24-33
+  if (mult == 0) return n;
+  const uint64_t r = n % mult;
+  return r ? n + mult - r : n;
+}
+
+uint64_t clamp_valid(uint64_t size, uint64_t start, uint64_t bs) {
+  if (size <= start) return 0;
+  return std::min<uint64_t>(size - start, bs);
+}
+
+}  // namespace
+
+// Coder::checkParams per class (rscoding.cpp:29-34, cauchycoding.cpp:30-35,
+// liberationcoding.cpp:29-36, irscoding.cpp:32-37) and the factory's
+// "Invalid Coding" (leo_erasure_nif.cpp:44-72).
+int check_params(int coding, int k, int m, int w) {
+  switch (coding) {
+    case LEOEC_VANDRS:
+      if (k <= 0 || m <= 0 || w <= 0) return LEOEC_E_PARAMS;
+      if (w != 8 && w != 16 && w != 32) return LEOEC_E_PARAMS_W_RS;
+      if (w == 8 && k + m > 256) return LEOEC_E_UNSUPPORTED;  // Jerasure: no matrix (NULL)
+      return LEOEC_OK;
+    case LEOEC_CAUCHYRS:
+      if (k <= 0 || m <= 0 || w <= 0) return LEOEC_E_PARAMS;
+      if (w < 31 && (long long)(k + m) > (1ll << w)) return LEOEC_E_PARAMS_LARGER_W;
+      if (w > 32) return LEOEC_E_UNSUPPORTED;
+      return LEOEC_OK;
+    case LEOEC_LIBERATION:
+      if (k <= 0 || m != 2 || w <= 0) return LEOEC_E_PARAMS_M2;
+      if (k > w) return LEOEC_E_PARAMS_K_LE_W;
+      if (w <= 2 || !(w % 2) || !is_prime_ref(w)) return LEOEC_E_PARAMS_W_PRIME;
+      if (w > 32) return LEOEC_E_UNSUPPORTED;
+      return LEOEC_OK;
+    case LEOEC_ISARS:
+      if (k <= 0 || m <= 0 || w <= 0) return LEOEC_E_PARAMS;
+      if (w != 8) return LEOEC_E_PARAMS_W8;
+      if (k + m > 256) return LEOEC_E_UNSUPPORTED;
+      return LEOEC_OK;
+    default:
+      return LEOEC_E_INVALID_CODING;
+  }
+}
+
+int get_code(int coding, int k, int m, int w, const Code** out) {
+  int rc = check_params(coding, k, m, w);
+  if (rc) return rc;
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int, int>, std::unique_ptr<Code>> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto key = std::make_tuple(coding, k, m, w);
+  auto it = cache.find(key);
+  if (it != cache.end()) {
+    *out = it->second.get();
+    return LEOEC_OK;
+  }
+  std::unique_ptr<Code> c(new Code);
+  c->coding = coding; c->k = k; c->m = m; c->w = w;
+  switch (coding) {
+    case LEOEC_VANDRS:
+      rc = vandermonde_coding_matrix(k, m, w, &c->C);
+      break;
+    case LEOEC_ISARS:
+      rc = isal_cauchy1_coding_matrix(k, m, &c->C);
+      break;
+    case LEOEC_CAUCHYRS:
+      c->bitmatrix = true;
+      rc = cauchy_good_coding_matrix(k, m, w, &c->C);
+      if (!rc) expand_to_bitmatrix(c->C, w, &c->B);
+      break;
+    case LEOEC_LIBERATION:
+      c->bitmatrix = true;
+      rc = liberation_coding_bitmatrix(k, w, &c->B);
+      break;
+  }
+  if (rc) return rc;
+  *out = c.get();
+  cache.emplace(key, std::move(c));
+  return LEOEC_OK;
+}
+
+// Decoding maps.  With G_S the k rows of the generator [I; C] for the
+// survivors S, the wanted block d (< k) is row d of G_S^-1 and a wanted
+// coding block p is C[p-k] * G_S^-1.  This is the linear map of
+// jerasure_make_decoding_matrix + jerasure_matrix_decode_data / _selected
+// (rscoding.cpp:147,198), of IRSCoding::gf_gen_decode_matrix
+// (irscoding.cpp:188-220) and, over GF(2), of the lazy schedule decoders
+// (cauchycoding.cpp:149,199; liberationcoding.cpp:147,195): for the same
+// survivor set it is the same map, so outputs agree bit for bit.
+int gf_rows(const Code& c, const int* surv, const int* want, int nwant,
+            std::vector<uint32_t>* rows) {
+  const int k = c.k;
+  const Field& F = field(c.w);
+  bool identity = true;
+  for (int i = 0; i < k; ++i) identity &= surv[i] == i;
+  GfMatrix inv;
+  if (!identity) {
+    GfMatrix G;
+    G.rows = G.cols = k;
+    G.a.assign((size_t)k * k, 0);
+    for (int i = 0; i < k; ++i) {
+      if (surv[i] < k) G.at(i, surv[i]) = 1;
+      else for (int j = 0; j < k; ++j) G.at(i, j) = c.C.at(surv[i] - k, j);
+    }
+    const int rc = gf_invert(G, c.w, &inv);
+    if (rc) return rc;
+  }
+  rows->assign((size_t)nwant * k, 0);
+  for (int o = 0; o < nwant; ++o) {
+    uint32_t* row = rows->data() + (size_t)o * k;
+    const int id = want[o];
+    if (id < k) {
+      if (identity) row[id] = 1;
+      else for (int j = 0; j < k; ++j) row[j] = inv.at(id, j);
+    } else if (identity) {
+      for (int j = 0; j < k; ++j) row[j] = c.C.at(id - k, j);
+    } else {
+      for (int j = 0; j < k; ++j) {
+        uint32_t acc = 0;
+        for (int l = 0; l < k; ++l) acc ^= F.mul(c.C.at(id - k, l), inv.at(l, j));
+        row[j] = acc;
+      }
+    }
+  }
+  return LEOEC_OK;
+}
+
+int bit_rows(const Code& c, const int* surv, const int* want, int nwant,
+             std::vector<uint8_t>* rows) {
+  const int k = c.k, w = c.w, n = k * w;
+  BitMatrix G, inv;
+  G.resize(n, n);
+  for (int i = 0; i < k; ++i)
+    for (int r = 0; r < w; ++r) {
+      if (surv[i] < k) {
+        G.set(i * w + r, surv[i] * w + r, true);
+      } else {
+        const uint64_t* src = c.B.row((surv[i] - k) * w + r);
+        std::copy(src, src + G.words, G.row(i * w + r));
+      }
+    }
+  const int rc = bit_invert(G, &inv);
+  if (rc) return rc;
+  rows->assign((size_t)nwant * w * n, 0);
+  std::vector<uint64_t> acc(inv.words);
+  for (int o = 0; o < nwant; ++o)
+    for (int r = 0; r < w; ++r) {
+      uint8_t* dst = rows->data() + (size_t)(o * w + r) * n;
+      if (want[o] < k) {
+        const int row = want[o] * w + r;
+        for (int col = 0; col < n; ++col) dst[col] = inv.get(row, col);
+      } else {
+        std::fill(acc.begin(), acc.end(), 0);
+        const int brow = (want[o] - k) * w + r;
+        for (int l = 0; l < n; ++l)
+          if (c.B.get(brow, l))
+            for (int x = 0; x < inv.words; ++x) acc[x] ^= inv.row(l)[x];
+        for (int col = 0; col < n; ++col) dst[col] = (acc[col / 64] >> (col % 64)) & 1;
+      }
+    }
+  return LEOEC_OK;
+}
+
+int apply(const Code& c, const int* surv, const std::vector<Shard>& in, const int* want,
+          const std::vector<Shard>& out, uint64_t bs, uint64_t nobj, hipStream_t s) {
+  const int nwant = (int)out.size();
+  if (nwant == 0 || nobj == 0 || bs == 0) return LEOEC_OK;
+  if (!c.bitmatrix) {
+    GfApply p;
+    p.w = c.w;
+    p.K = c.k;
+    p.R = nwant;
+    int rc = gf_rows(c, surv, want, nwant, &p.coef);
+    if (rc) return rc;
+    p.in = in;
+    p.out = out;
+    p.block_size = bs;
+    p.nobj = nobj;
+    return launch(p, s);
+  }
+  BitApply p;
+  p.w = c.w;
+  p.KB = c.k;
+  p.RB = nwant;
+  int rc = bit_rows(c, surv, want, nwant, &p.bits);
+  if (rc) return rc;
+  p.in = in;
+  p.out = out;
+  p.block_size = bs;
+  p.nobj = nobj;
+  return launch(p, s);
+}
+
+// ---------------------------------------------------------------------------
+// Device and per-thread staging.
+int device_init() {
+  static std::once_flag once;
+  static int status = LEOEC_E_NO_DEVICE;
+  std::call_once(once, [] {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return;
+    status = LEOEC_OK;
+  });
+  return status;
+}
+
+namespace {
+
+struct Staging {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  uint8_t* buf = nullptr;
+  size_t cap = 0;
+};
+
+thread_local Staging tl_staging;  // one stream + device buffer per calling thread
+
+int get_staging(size_t bytes, Staging** out) {
+  int rc = device_init();
+  if (rc) return rc;
+  Staging& st = tl_staging;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return LEOEC_E_HIP;
+  if (st.device != dev) {
+    st = Staging();
+    if (hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking) != hipSuccess)
+      return LEOEC_E_HIP;
+    st.device = dev;
+  }
+  if (st.cap < bytes) {
+    if (st.buf) {
+      (void)hipStreamSynchronize(st.stream);
+      (void)hipFree(st.buf);
+      st.buf = nullptr;
+      st.cap = 0;
+    }
+    const size_t want = std::max<size_t>(bytes + bytes / 4, (size_t)1 << 20);
+    if (hipMalloc(&st.buf, want) != hipSuccess) return LEOEC_E_NOMEM;
+    st.cap = want;
+  }
+  *out = &st;
+  return LEOEC_OK;
+}
+
+// Reference-order validation of (blocks, ids): ids in range, >= k unique,
+// no duplicates (rscoding.cpp:89-94; the set-size tests come first).
+int index_blocks(int k, int m, const int* ids, int n, std::vector<int>* present) {
+  present->assign(k + m, -1);
+  int uniq = 0;
+  for (int i = 0; i < n; ++i) {
+    if (ids[i] < 0 || ids[i] >= k + m) return LEOEC_E_BAD_ID;
+    if ((*present)[ids[i]] < 0) ++uniq;
+    (*present)[ids[i]] = i;
+  }
+  if (uniq < k) return LEOEC_E_NOT_ENOUGH_BLOCKS;
+  if (uniq < n) return LEOEC_E_NOT_UNIQUE;
+  return LEOEC_OK;
+}
+
+// Survivors: Jerasure decodes from the first k intact ids in ascending order
+// (jerasure_make_decoding_matrix's dm_ids / set_up_ids_for_scheduled_decoding);
+// ISA-L's decode matrix uses the first k blocks as listed (irscoding.cpp:193-197).
+void pick_survivors(int coding, int k, const int* ids, const std::vector<int>& present,
+                    std::vector<int>* surv, std::vector<int>* slot) {
+  surv->clear();
+  slot->clear();
+  if (coding == LEOEC_ISARS) {
+    for (int i = 0; i < k; ++i) { surv->push_back(ids[i]); slot->push_back(i); }
+    return;
+  }
+  for (int id = 0; id < (int)present.size() && (int)surv->size() < k; ++id)
+    if (present[id] >= 0) { surv->push_back(id); slot->push_back(present[id]); }
+}
+
+int hip_ok(hipError_t e) { return e == hipSuccess ? LEOEC_OK : LEOEC_E_HIP; }
+
+// Stage the k survivor blocks, run the map into nwant device outputs.
+int run_host_map(const Code& c, const uint8_t* const* blocks, const std::vector<int>& surv,
+                 const std::vector<int>& slot, const std::vector<int>& want, uint64_t bs,
+                 Staging** st_out, uint8_t** dev_out, uint64_t* stride_out) {
+  const int k = c.k;
+  const uint64_t bs16 = round_to(bs, 16);
+  if (c.bitmatrix && (bs % (16ull * (uint64_t)c.w))) return LEOEC_E_BAD_SIZE;
+  Staging* st;
+  int rc = get_staging((size_t)(k + want.size()) * bs16, &st);
+  if (rc) return rc;
+  std::vector<Shard> in(k), out(want.size());
+  for (int i = 0; i < k; ++i) {
+    uint8_t* dst = st->buf + (uint64_t)i * bs16;
+    rc = hip_ok(hipMemcpyAsync(dst, blocks[slot[i]], bs, hipMemcpyHostToDevice, st->stream));
+    if (rc) return rc;
+    in[i] = Shard{dst, 0, bs};
+  }
+  uint8_t* outbase = st->buf + (uint64_t)k * bs16;
+  for (size_t o = 0; o < want.size(); ++o) out[o] = Shard{outbase + o * bs16, 0, bs};
+  rc = apply(c, surv.data(), in, want.data(), out, bs16, 1, st->stream);
+  if (rc) return rc;
+  *st_out = st;
+  *dev_out = outbase;
+  *stride_out = bs16;
+  return LEOEC_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+int op_layout(int coding, int k, int m, int w, uint64_t size, uint64_t* bs, int* filled) {
+  int rc = check_params(coding, k, m, w);
+  if (rc) return rc;
+  // rscoding.cpp:44 (identical in every coder)
+  const uint64_t kw = (uint64_t)k * (uint64_t)w;
+  const uint64_t b = round_to(round_to(size, kw) / kw, 16) * (uint64_t)w;
+  if (bs) *bs = b;
+  if (filled) {
+    // rscoding.cpp:49-54: whole blocks that alias the input.  (For an empty
+    // object the reference loops forever; here nothing aliases.)
+    uint64_t f = b ? size / b : 0;
+    *filled = (int)std::min<uint64_t>(f, (uint64_t)k);
+  }
+  return LEOEC_OK;
+}
+
+// RSCoding::doEncode (rscoding.cpp:36-85) and siblings.  `out` receives the
+// bytes of the reference's fresh binary: zero-padded tail data block(s),
+// then the m coding blocks.
+int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size, uint8_t* out,
+              uint64_t out_size) {
+  uint64_t bs;
+  int filled;
+  int rc = op_layout(coding, k, m, w, size, &bs, &filled);
+  if (rc) return rc;
+  const uint64_t need = (uint64_t)(k + m - filled) * bs;
+  if (out_size < need || (size && !obj) || (need && !out)) return LEOEC_E_ARG;
+  if (bs == 0) return LEOEC_OK;
+  const Code* c;
+  rc = get_code(coding, k, m, w, &c);
+  if (rc) return rc;
+  if (bs >= (1ull << 32)) return LEOEC_E_BAD_SIZE;
+  // tail data blocks: zero-filled, tail bytes copied (rscoding.cpp:55-65)
+  const uint64_t tail_bytes = (uint64_t)(k - filled) * bs;
+  std::memset(out, 0, tail_bytes);
+  std::memcpy(out, obj + (uint64_t)filled * bs, size - (uint64_t)filled * bs);
+
+  Staging* st;
+  rc = get_staging((size_t)(k + m) * bs, &st);
+  if (rc) return rc;
+  rc = hip_ok(hipMemcpyAsync(st->buf, obj, size, hipMemcpyHostToDevice, st->stream));
+  if (rc) return rc;
+  std::vector<Shard> in(k), par(m);
+  std::vector<int> surv(k), want(m);
+  for (int j = 0; j < k; ++j) {
+    in[j] = Shard{st->buf + (uint64_t)j * bs, 0, clamp_valid(size, (uint64_t)j * bs, bs)};
+    surv[j] = j;
+  }
+  for (int i = 0; i < m; ++i) {
+    par[i] = Shard{st->buf + (uint64_t)(k + i) * bs, 0, bs};
+    want[i] = k + i;
+  }
+  rc = apply(*c, surv.data(), in, want.data(), par, bs, 1, st->stream);
+  if (rc) return rc;
+  rc = hip_ok(hipMemcpyAsync(out + tail_bytes, st->buf + (uint64_t)k * bs, (uint64_t)m * bs,
+                             hipMemcpyDeviceToHost, st->stream));
+  if (rc) return rc;
+  return hip_ok(hipStreamSynchronize(st->stream));
+}
+
+// doDecode (rscoding.cpp:87-154 and siblings): output = first `size` bytes
+// of D0..Dk-1.  The all-data fast path is a host copy, as in the reference.
+int op_decode(int coding, int k, int m, int w, const uint8_t* const* blocks, const int* ids, int n,
+              uint64_t bs, uint64_t size, uint8_t* out) {
+  int rc = check_params(coding, k, m, w);
+  if (rc) return rc;
+  if (n < 0 || (n && (!blocks || !ids)) || (size && !out)) return LEOEC_E_ARG;
+  std::vector<int> present;
+  rc = index_blocks(k, m, ids, n, &present);
+  if (rc) return rc;
+  if (size > (uint64_t)k * bs) return LEOEC_E_BAD_SIZE;
+  for (int i = 0; i < n; ++i)
+    if (!blocks[i]) return LEOEC_E_ARG;
+  std::vector<int> want;
+  for (int i = 0; i < k; ++i)
+    if (present[i] < 0 && (uint64_t)i * bs < size) want.push_back(i);
+  Staging* st = nullptr;
+  uint8_t* dev = nullptr;
+  uint64_t dstride = 0;
+  if (!want.empty()) {
+    const Code* c;
+    rc = get_code(coding, k, m, w, &c);
+    if (rc) return rc;
+    std::vector<int> surv, slot;
+    pick_survivors(coding, k, ids, present, &surv, &slot);
+    rc = run_host_map(*c, blocks, surv, slot, want, bs, &st, &dev, &dstride);
+    if (rc) return rc;
+    for (size_t o = 0; o < want.size(); ++o) {
+      const uint64_t off = (uint64_t)want[o] * bs;
+      rc = hip_ok(hipMemcpyAsync(out + off, dev + o * dstride, clamp_valid(size, off, bs),
+                                 hipMemcpyDeviceToHost, st->stream));
+      if (rc) return rc;
+    }
+  }
+  for (int i = 0; i < k; ++i) {
+    const uint64_t off = (uint64_t)i * bs;
+    if (off >= size) break;
+    if (present[i] >= 0) std::memcpy(out + off, blocks[present[i]], clamp_valid(size, off, bs));
+  }
+  if (st) return hip_ok(hipStreamSynchronize(st->stream));
+  return LEOEC_OK;
+}
+
+// doRepair (rscoding.cpp:156-211 and siblings): blocks in repair-list order.
+int op_repair(int coding, int k, int m, int w, const uint8_t* const* blocks, const int* ids, int n,
+              uint64_t bs, const int* rep, int nrep, uint8_t* out) {
+  int rc = check_params(coding, k, m, w);
+  if (rc) return rc;
+  if (n < 0 || nrep < 0 || (n && (!blocks || !ids)) || (nrep && (!rep || !out)))
+    return LEOEC_E_ARG;
+  std::vector<int> present;
+  rc = index_blocks(k, m, ids, n, &present);
+  if (rc) return rc;
+  for (int i = 0; i < n; ++i)
+    if (!blocks[i]) return LEOEC_E_ARG;
+  std::vector<int> want, pos;
+  for (int r = 0; r < nrep; ++r) {
+    if (rep[r] < 0 || rep[r] >= k + m) return LEOEC_E_BAD_ID;
+    // Jerasure leaves an intact selected block as it was staged; ISA-L
+    // recomputes every requested row (irscoding.cpp:171-176).
+    if (coding != LEOEC_ISARS && present[rep[r]] >= 0) {
+      std::memcpy(out + (uint64_t)r * bs, blocks[present[rep[r]]], bs);
+    } else {
+      want.push_back(rep[r]);
+      pos.push_back(r);
+    }
+  }
+  if (want.empty() || bs == 0) return LEOEC_OK;
+  const Code* c;
+  rc = get_code(coding, k, m, w, &c);
+  if (rc) return rc;
+  std::vector<int> surv, slot;
+  pick_survivors(coding, k, ids, present, &surv, &slot);
+  Staging* st;
+  uint8_t* dev;
+  uint64_t dstride;
+  rc = run_host_map(*c, blocks, surv, slot, want, bs, &st, &dev, &dstride);
+  if (rc) return rc;
+  for (size_t o = 0; o < want.size(); ++o) {
+    rc = hip_ok(hipMemcpyAsync(out + (uint64_t)pos[o] * bs, dev + o * dstride, bs,
+                               hipMemcpyDeviceToHost, st->stream));
+    if (rc) return rc;
+  }
+  return hip_ok(hipStreamSynchronize(st->stream));
+}
+
+// ---------------------------------------------------------------------------
+// Device-resident batched operations.
+int op_encode_dev(int coding, int k, int m, int w, const uint8_t* objs, uint64_t obj_stride,
+                  uint64_t size, uint64_t nobj, uint8_t* parity, uint64_t parity_stride,
+                  hipStream_t s) {
+  uint64_t bs;
+  int rc = op_layout(coding, k, m, w, size, &bs, nullptr);
+  if (rc) return rc;
+  if (nobj == 0 || bs == 0) return LEOEC_OK;
+  if (!objs || !parity) return LEOEC_E_ARG;
+  if ((nobj > 1 && (obj_stride < size || parity_stride < (uint64_t)m * bs))) return LEOEC_E_ARG;
+  if ((rc = device_init())) return rc;
+  const Code* c;
+  if ((rc = get_code(coding, k, m, w, &c))) return rc;
+  std::vector<Shard> in(k), par(m);
+  std::vector<int> surv(k), want(m);
+  for (int j = 0; j < k; ++j) {
+    in[j] = Shard{objs + (uint64_t)j * bs, obj_stride, clamp_valid(size, (uint64_t)j * bs, bs)};
+    surv[j] = j;
+  }
+  for (int i = 0; i < m; ++i) {
+    par[i] = Shard{parity + (uint64_t)i * bs, parity_stride, bs};
+    want[i] = k + i;
+  }
+  return apply(*c, surv.data(), in, want.data(), par, bs, nobj, s);
+}
+
+int op_decode_dev(int coding, int k, int m, int w, uint8_t* objs, uint64_t obj_stride,
+                  uint64_t size, uint64_t nobj, const uint8_t* parity, uint64_t parity_stride,
+                  const int* erased, int nerased, hipStream_t s) {
+  uint64_t bs;
+  int rc = op_layout(coding, k, m, w, size, &bs, nullptr);
+  if (rc) return rc;
+  if (nerased < 0 || (nerased && !erased)) return LEOEC_E_ARG;
+  std::vector<char> gone(k + m, 0);
+  for (int i = 0; i < nerased; ++i) {
+    if (erased[i] < 0 || erased[i] >= k + m) return LEOEC_E_BAD_ID;
+    gone[erased[i]] = 1;
+  }
+  std::vector<int> surv, want;
+  for (int id = 0; id < k + m && (int)surv.size() < k; ++id)
+    if (!gone[id]) surv.push_back(id);
+  if ((int)surv.size() < k) return LEOEC_E_NOT_ENOUGH_BLOCKS;
+  for (int id = 0; id < k; ++id)
+    if (gone[id] && (uint64_t)id * bs < size) want.push_back(id);
+  if (want.empty() || nobj == 0 || bs == 0) return LEOEC_OK;
+  if (!objs || !parity) return LEOEC_E_ARG;
+  if ((rc = device_init())) return rc;
+  const Code* c;
+  if ((rc = get_code(coding, k, m, w, &c))) return rc;
+  std::vector<Shard> in(k), out(want.size());
+  for (int i = 0; i < k; ++i) {
+    const int id = surv[i];
+    if (id < k)
+      in[i] = Shard{objs + (uint64_t)id * bs, obj_stride, clamp_valid(size, (uint64_t)id * bs, bs)};
+    else
+      in[i] = Shard{parity + (uint64_t)(id - k) * bs, parity_stride, bs};
+  }
+  for (size_t o = 0; o < want.size(); ++o)
+    out[o] = Shard{objs + (uint64_t)want[o] * bs, obj_stride,
+                   clamp_valid(size, (uint64_t)want[o] * bs, bs)};
+  return apply(*c, surv.data(), in, want.data(), out, bs, nobj, s);
+}
+
+int op_repair_dev(int coding, int k, int m, int w, const uint8_t* const* blocks,
+                  uint64_t block_stride, uint64_t bs, uint64_t nobj, const int* rep, int nrep,
+                  uint8_t* const* out, uint64_t out_stride, hipStream_t s) {
+  int rc = check_params(coding, k, m, w);
+  if (rc) return rc;
+  if (!blocks || nrep < 0 || (nrep && (!rep || !out))) return LEOEC_E_ARG;
+  std::vector<int> surv;
+  for (int id = 0; id < k + m && (int)surv.size() < k; ++id)
+    if (blocks[id]) surv.push_back(id);
+  if ((int)surv.size() < k) return LEOEC_E_NOT_ENOUGH_BLOCKS;
+  std::vector<int> want(rep, rep + nrep);
+  for (int r = 0; r < nrep; ++r) {
+    if (rep[r] < 0 || rep[r] >= k + m) return LEOEC_E_BAD_ID;
+    if (!out[r]) return LEOEC_E_ARG;
+  }
+  if (nrep == 0 || nobj == 0 || bs == 0) return LEOEC_OK;
+  if ((rc = device_init())) return rc;
+  const Code* c;
+  if ((rc = get_code(coding, k, m, w, &c))) return rc;
+  std::vector<Shard> in(k), o(nrep);
+  for (int i = 0; i < k; ++i) in[i] = Shard{blocks[surv[i]], block_stride, bs};
+  for (int r = 0; r < nrep; ++r) o[r] = Shard{out[r], out_stride, bs};
+  return apply(*c, surv.data(), in, want.data(), o, bs, nobj, s);
+}
+
+}  // namespace leoec

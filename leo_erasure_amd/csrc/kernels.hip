@@ -1,0 +1,135 @@
+// kernels.hip — dispatch of GfApply / BitApply plans onto the gfx950 kernels
+// of kernels_impl.hpp (w = 16/32 and bitmatrix instances live here; GF(2^8)
+// instances in gf8_inst.hip).
+#include <utility>
+
+#include "kernels_impl.hpp"
+
+namespace leoec {
+
+using namespace detail;
+
+namespace {
+
+bool shards_ok(const std::vector<Shard>& v) {
+  for (const Shard& s : v)
+    if (((uintptr_t)s.base & 15u) || (s.stride & 15u)) return false;
+  return true;
+}
+
+template <std::size_t... I>
+ChunkFn gf8_pick(std::index_sequence<I...>, int k, int r, bool acc) {
+  static ChunkFn (*const sel[])(int, bool) = {&gf8_launcher<(int)I + 1>...};
+  return sel[k - 1](r, acc);
+}
+
+template <int W>
+ChunkFn gfw_pick(int r, bool acc) {
+  static const ChunkFn tbl[2][kMaxR] = {
+      {&launch_gfw_t<W, 1, false>, &launch_gfw_t<W, 2, false>, &launch_gfw_t<W, 3, false>,
+       &launch_gfw_t<W, 4, false>},
+      {&launch_gfw_t<W, 1, true>, &launch_gfw_t<W, 2, true>, &launch_gfw_t<W, 3, true>,
+       &launch_gfw_t<W, 4, true>}};
+  return tbl[acc ? 1 : 0][r - 1];
+}
+
+}  // namespace
+
+int launch(const GfApply& p, hipStream_t s) {
+  if (p.K <= 0 || p.R <= 0 || (int)p.in.size() != p.K || (int)p.out.size() != p.R ||
+      p.coef.size() != (size_t)p.K * p.R)
+    return LEOEC_E_ARG;
+  if (p.w != 8 && p.w != 16 && p.w != 32) return LEOEC_E_UNSUPPORTED;
+  if (p.block_size == 0 || p.nobj == 0) return LEOEC_OK;
+  if ((p.block_size & 15u) || p.block_size >= (1ull << 32)) return LEOEC_E_BAD_SIZE;
+  if (!shards_ok(p.in) || !shards_ok(p.out)) return LEOEC_E_ARG;
+  const uint32_t tiles = (uint32_t)((p.block_size + kTileBytes - 1) / kTileBytes);
+  const uint64_t max_obj = (uint64_t)0x7FFFFFFF / tiles;
+  for (uint64_t o0 = 0; o0 < p.nobj; o0 += max_obj) {
+    const uint64_t no = (p.nobj - o0 < max_obj) ? p.nobj - o0 : max_obj;
+    for (int r0 = 0; r0 < p.R; r0 += kMaxR) {
+      const int nr = (p.R - r0 < kMaxR) ? p.R - r0 : kMaxR;
+      // inputs beyond 16 are folded in by accumulating launches (ACC)
+      for (int j0 = 0; j0 < p.K; j0 += kMaxK) {
+        const int nk = (p.K - j0 < kMaxK) ? p.K - j0 : kMaxK;
+        const Chunk c{r0, nr, j0, nk, o0, no, tiles};
+        ChunkFn fn;
+        if (p.w == 8)
+          fn = gf8_pick(std::make_index_sequence<kMaxK>{}, nk, nr, j0 > 0);
+        else if (p.w == 16)
+          fn = gfw_pick<16>(nr, j0 > 0);
+        else
+          fn = gfw_pick<32>(nr, j0 > 0);
+        const int rc = fn(p, c, s);
+        if (rc) return rc;
+      }
+    }
+  }
+  return LEOEC_OK;
+}
+
+int launch(const BitApply& p, hipStream_t s) {
+  const int w = p.w;
+  if (w <= 0 || w > 32 || p.KB <= 0 || p.RB <= 0 || (int)p.in.size() != p.KB ||
+      (int)p.out.size() != p.RB || p.bits.size() != (size_t)p.RB * w * p.KB * w)
+    return LEOEC_E_ARG;
+  if (p.block_size == 0 || p.nobj == 0) return LEOEC_OK;
+  if (p.block_size % ((uint64_t)16 * w) || p.block_size >= (1ull << 32)) return LEOEC_E_BAD_SIZE;
+  if (!shards_ok(p.in) || !shards_ok(p.out)) return LEOEC_E_ARG;
+  const uint32_t ps = (uint32_t)(p.block_size / (uint64_t)w);
+  const uint32_t tiles = (ps + kTileBytes - 1) / kTileBytes;
+  const uint64_t max_obj = (uint64_t)0x7FFFFFFF / tiles;
+  const int blocks_per_pass = kMaxPk / w;  // output blocks whose packets fit one launch
+  const int KPtot = p.KB * w;
+  for (uint64_t o0 = 0; o0 < p.nobj; o0 += max_obj) {
+    const uint64_t no = (p.nobj - o0 < max_obj) ? p.nobj - o0 : max_obj;
+    for (int b0 = 0; b0 < p.RB; b0 += blocks_per_pass) {
+      const int nb = (p.RB - b0 < blocks_per_pass) ? p.RB - b0 : blocks_per_pass;
+      const int RP = nb * w;
+      for (int j0 = 0; j0 < p.KB; j0 += kMaxK) {
+        const int nk = (p.KB - j0 < kMaxK) ? p.KB - j0 : kMaxK;
+        BitArgs a;
+        a.w = w;
+        a.KP = nk * w;
+        a.ps = ps;
+        a.tiles = tiles;
+        for (int j = 0; j < kMaxK; ++j)
+          a.in[j] = j < nk ? dev_shard(p.in[j0 + j], o0) : DevShard{nullptr, 0, 0, 0};
+        for (int o = 0; o < kMaxPk; ++o) {
+          a.out[o] = DevShard{nullptr, 0, 0, 0};
+          if (o >= RP) continue;
+          const Shard& sh = p.out[b0 + o / w];
+          const uint64_t pk = (uint64_t)(o % w) * ps;
+          DevShard d = dev_shard(sh, o0);
+          d.base += pk;
+          const uint64_t v = sh.valid > pk ? sh.valid - pk : 0;
+          d.valid = (uint32_t)(v < ps ? v : ps);
+          a.out[o] = d;
+        }
+        for (int q = 0; q < kMaxK * 32; ++q) {
+          uint32_t word = 0;
+          if (q < nk * w)
+            for (int o = 0; o < RP; ++o)
+              if (p.bits[(size_t)(b0 * w + o) * KPtot + (size_t)j0 * w + q]) word |= 1u << (31 - o);
+          a.bits[q] = word;
+        }
+        const bool acc = j0 > 0;
+        const dim3 grid((uint32_t)(no * tiles)), block(kThreads);
+        if (RP <= 8) {
+          if (acc) hipLaunchKernelGGL((bit_apply<8, true>), grid, block, 0, s, a);
+          else hipLaunchKernelGGL((bit_apply<8, false>), grid, block, 0, s, a);
+        } else if (RP <= 16) {
+          if (acc) hipLaunchKernelGGL((bit_apply<16, true>), grid, block, 0, s, a);
+          else hipLaunchKernelGGL((bit_apply<16, false>), grid, block, 0, s, a);
+        } else {
+          if (acc) hipLaunchKernelGGL((bit_apply<32, true>), grid, block, 0, s, a);
+          else hipLaunchKernelGGL((bit_apply<32, false>), grid, block, 0, s, a);
+        }
+        if (hipGetLastError() != hipSuccess) return LEOEC_E_HIP;
+      }
+    }
+  }
+  return LEOEC_OK;
+}
+
+}  // namespace leoec

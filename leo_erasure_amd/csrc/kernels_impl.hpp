@@ -1,0 +1,393 @@
+// kernels_impl.hpp — gfx950 (CDNA4) kernels of the erasure-coding engine and
+// their launch templates.  Included by kernels.hip (dispatch, w=16/32 and
+// bitmatrix instances) and gf8_inst.hip (GF(2^8) instances, one translation
+// unit per input count K so the 128 unrolled variants build in parallel).
+//
+// The work is memory-bound byte / XOR arithmetic: no MFMA and no LDS.  Each
+// lane owns one 16-byte column of a block and walks down the K input blocks
+// with global_load_dwordx4 (one wave reads 1 KiB contiguous per block: fully
+// coalesced), keeps its R output columns in VGPRs and stores each once, so
+// every input byte is read from HBM once and every output byte written once.
+//
+// GF(2^8) multiply by a wave-uniform constant c uses v_perm_b32 as an 8-entry
+// byte-table lookup (four lookups per instruction):
+//     c*x = T0[x & 7] ^ T1[(x >> 3) & 7] ^ T2[x >> 6]
+// with T0[i] = c*i, T1[i] = c*(i<<3), T2[i] = c*(i<<6) (poly 0x11D).  The three
+// selector dwords of a data dword are shared by every output row; per
+// coefficient a dword costs 3 v_perm + v_bitop3 (xor3) + v_xor.  Coefficients
+// 0 and 1 take a scalar branch (skip / plain xor).  The 5 table dwords per
+// coefficient are kernel arguments, read by s_load into SGPRs.
+//
+// GF(2^16) / GF(2^32) use shift-and-add: x*2^b is formed once per input word
+// and masked into every row whose coefficient has bit b (v_bitop3 a^(b&c)).
+//
+// Bitmatrix codes (cauchyrs, liberation) are a GF(2) matrix over packets of
+// block_size / w bytes: out packet o ^= in packet p & mask(o, p), the 0/~0
+// masks taken from one uniform bit word per input packet.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/leoec.h"
+#include "kernels.hpp"
+
+namespace leoec {
+namespace detail {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr uint32_t kTileBytes = kThreads * 16;  // one 16-byte column per lane
+constexpr int kMaxK = 16;                       // input blocks per launch
+constexpr int kMaxR = 4;                        // GF output blocks per launch
+constexpr int kMaxPk = 32;                      // bitmatrix output packets per launch
+
+struct DevShard {
+  const uint8_t* base;
+  uint64_t stride;
+  uint32_t valid;
+  uint32_t pad;
+};
+
+// One launch covers objects [o0, o0+no) and output rows / input columns
+// [r0, r0+nr) x [j0, j0+nk) of the plan; tiles = 4 KiB tiles per block.
+struct Chunk {
+  int r0, nr, j0, nk;
+  uint64_t o0, no;
+  uint32_t tiles;
+};
+
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Bytes of v at index >= n (0 <= n < 16) cleared.
+__device__ __forceinline__ u32x4 keep_first(u32x4 v, uint32_t n) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t lo = 4u * e;
+    const uint32_t m = n >= lo + 4u ? 0xFFFFFFFFu : (n <= lo ? 0u : (1u << (8u * (n - lo))) - 1u);
+    v[e] &= m;
+  }
+  return v;
+}
+
+// Guarded load for tiles that cross a block's valid length: a chunk whose
+// first byte is valid is read whole (an aligned 16-byte chunk never crosses a
+// page) and its bytes past `valid` cleared; chunks past `valid` are not read.
+__device__ __forceinline__ u32x4 load_guarded(const uint8_t* p, uint32_t off, uint32_t valid) {
+  u32x4 v = {0u, 0u, 0u, 0u};
+  if (off < valid) v = *reinterpret_cast<const u32x4*>(p + off);
+  if (off + 16u > valid) v = keep_first(v, off < valid ? valid - off : 0u);
+  return v;
+}
+
+// Guarded store: never writes a byte at or past `valid`.
+__device__ __forceinline__ void store_guarded(uint8_t* p, uint32_t off, uint32_t valid, u32x4 v) {
+  if (off + 16u <= valid) {
+    *reinterpret_cast<u32x4*>(p + off) = v;
+  } else if (off < valid) {
+    const uint32_t n = valid - off;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if ((uint32_t)i < n) p[off + i] = (uint8_t)(v[i >> 2] >> (8 * (i & 3)));
+  }
+}
+
+// ===========================================================================
+// GF(2^8): K inputs x R outputs, fully unrolled.
+template <int K, int R>
+struct Gf8Args {
+  DevShard in[K];
+  DevShard out[R];
+  uint32_t tab[R][K][5];  // T0 lo, T0 hi, T1 lo, T1 hi, T2
+  uint64_t one;           // bit r*K+j set: coefficient is 1
+  uint64_t zero;          // bit r*K+j set: coefficient is 0
+  uint32_t tiles;         // tiles per object
+  uint32_t vmin;          // min valid over all shards of the launch
+};
+
+template <int K, int R, bool ACC>
+__global__ void __launch_bounds__(kThreads) gf8_apply(const Gf8Args<K, R> a) {
+  const uint32_t obj = blockIdx.x / a.tiles;
+  const uint32_t tile = blockIdx.x - obj * a.tiles;
+  const uint32_t t0 = tile * kTileBytes;
+  const uint32_t off = t0 + threadIdx.x * 16u;
+  const bool full = t0 + kTileBytes <= a.vmin;  // wave-uniform
+  const uint64_t o = obj;
+
+  u32x4 d[K];
+  if (full) {
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      d[j] = *reinterpret_cast<const u32x4*>(a.in[j].base + o * a.in[j].stride + off);
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      d[j] = load_guarded(a.in[j].base + o * a.in[j].stride, off, a.in[j].valid);
+  }
+  u32x4 acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    acc[r] = u32x4{0u, 0u, 0u, 0u};
+    if (ACC) acc[r] = load_guarded(a.out[r].base + o * a.out[r].stride, off, a.out[r].valid);
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    uint32_t s0[4], s1[4], s2[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t x = d[j][e];
+      s0[e] = x & 0x07070707u;
+      s1[e] = (x >> 3) & 0x07070707u;
+      s2[e] = (x >> 6) & 0x03030303u;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int bit = r * K + j;
+      if ((a.one >> bit) & 1) {
+        acc[r] ^= d[j];
+      } else if (!((a.zero >> bit) & 1)) {
+        const uint32_t t0l = a.tab[r][j][0], t0h = a.tab[r][j][1];
+        const uint32_t t1l = a.tab[r][j][2], t1h = a.tab[r][j][3];
+        const uint32_t t2 = a.tab[r][j][4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t p0 = perm(t0h, t0l, s0[e]);
+          const uint32_t p1 = perm(t1h, t1l, s1[e]);
+          const uint32_t p2 = perm(t2, t2, s2[e]);
+          acc[r][e] = xor3(acc[r][e], p0, p1) ^ p2;
+        }
+      }
+    }
+  }
+  if (full) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      *reinterpret_cast<u32x4*>(const_cast<uint8_t*>(a.out[r].base) + o * a.out[r].stride + off) =
+          acc[r];
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      store_guarded(const_cast<uint8_t*>(a.out[r].base) + o * a.out[r].stride, off,
+                    a.out[r].valid, acc[r]);
+  }
+}
+
+// ===========================================================================
+// GF(2^16) / GF(2^32): shift-and-add over little-endian words, K runtime.
+template <int R>
+struct GfwArgs {
+  DevShard in[kMaxK];
+  DevShard out[R];
+  uint32_t coef[R][kMaxK];
+  int K;
+  uint32_t tiles;
+  uint32_t vmin;
+};
+
+template <int W>
+__device__ __forceinline__ uint32_t xtime(uint32_t x) {
+  if (W == 32) {  // x^32 = x^22 + x^2 + x + 1
+    const uint32_t sign = (uint32_t)((int32_t)x >> 31);
+    return (x << 1) ^ (sign & 0x00400007u);
+  } else {  // two packed 16-bit words, x^16 = x^12 + x^3 + x + 1
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    typedef short s16x2 __attribute__((ext_vector_type(2)));
+    const u16x2 v = __builtin_bit_cast(u16x2, x);
+    const u16x2 sh = v << (unsigned short)1;
+    const s16x2 sg = __builtin_bit_cast(s16x2, v) >> (short)15;
+    return __builtin_bit_cast(uint32_t, sh) ^ (__builtin_bit_cast(uint32_t, sg) & 0x100B100Bu);
+  }
+}
+
+template <int W, int R, bool ACC>
+__global__ void __launch_bounds__(kThreads) gfw_apply(const GfwArgs<R> a) {
+  const uint32_t obj = blockIdx.x / a.tiles;
+  const uint32_t tile = blockIdx.x - obj * a.tiles;
+  const uint32_t t0 = tile * kTileBytes;
+  const uint32_t off = t0 + threadIdx.x * 16u;
+  const bool full = t0 + kTileBytes <= a.vmin;
+  const uint64_t o = obj;
+  u32x4 acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    acc[r] = u32x4{0u, 0u, 0u, 0u};
+    if (ACC) acc[r] = load_guarded(a.out[r].base + o * a.out[r].stride, off, a.out[r].valid);
+  }
+  for (int j = 0; j < a.K; ++j) {
+    const uint8_t* p = a.in[j].base + o * a.in[j].stride;
+    u32x4 x = full ? *reinterpret_cast<const u32x4*>(p + off) : load_guarded(p, off, a.in[j].valid);
+    uint32_t c[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) c[r] = a.coef[r][j];
+#pragma unroll
+    for (int b = 0; b < W; ++b) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint32_t m = (uint32_t)(-(int32_t)((c[r] >> b) & 1u));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[r][e] ^= x[e] & m;
+      }
+      if (b + 1 < W) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = xtime<W>(x[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    store_guarded(const_cast<uint8_t*>(a.out[r].base) + o * a.out[r].stride, off, a.out[r].valid,
+                  acc[r]);
+}
+
+// ===========================================================================
+// Bitmatrix (GF(2)) over packets of ps bytes.
+struct BitArgs {
+  DevShard in[kMaxK];
+  DevShard out[kMaxPk];        // one per output packet, base already at the packet
+  uint32_t bits[kMaxK * 32];   // per input packet: bit (31 - o) set => feeds output packet o
+  int w;
+  int KP;                      // input packets = input blocks * w
+  uint32_t ps;                 // packet bytes
+  uint32_t tiles;              // tiles per object (over one packet)
+};
+
+template <int RO, bool ACC>
+__global__ void __launch_bounds__(kThreads) bit_apply(const BitArgs a) {
+  const uint32_t obj = blockIdx.x / a.tiles;
+  const uint32_t tile = blockIdx.x - obj * a.tiles;
+  const uint32_t off = tile * kTileBytes + threadIdx.x * 16u;
+  if (off >= a.ps) return;
+  const uint64_t o64 = obj;
+  u32x4 acc[RO];
+#pragma unroll
+  for (int o = 0; o < RO; ++o) {
+    acc[o] = u32x4{0u, 0u, 0u, 0u};
+    if (ACC) acc[o] = load_guarded(a.out[o].base + o64 * a.out[o].stride, off, a.out[o].valid);
+  }
+  int blk = 0, x = 0;
+  for (int p = 0; p < a.KP; ++p) {
+    const uint32_t pk = (uint32_t)x * a.ps;
+    const uint32_t bv = a.in[blk].valid;
+    const uint32_t valid = bv > pk ? bv - pk : 0u;
+    const u32x4 v = load_guarded(a.in[blk].base + o64 * a.in[blk].stride + pk, off, valid);
+    const uint32_t bits = a.bits[p];
+#pragma unroll
+    for (int o = 0; o < RO; ++o) {
+      const uint32_t m = (uint32_t)((int32_t)(bits << o) >> 31);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[o][e] ^= v[e] & m;
+    }
+    if (++x == a.w) {
+      x = 0;
+      ++blk;
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < RO; ++o) {
+    uint8_t* p = const_cast<uint8_t*>(a.out[o].base);
+    if (p != nullptr) store_guarded(p + o64 * a.out[o].stride, off, a.out[o].valid, acc[o]);
+  }
+}
+
+// ===========================================================================
+// Host-side launch templates.
+inline DevShard dev_shard(const Shard& s, uint64_t o0) {
+  DevShard d;
+  d.base = s.base + o0 * s.stride;
+  d.stride = s.stride;
+  d.valid = (uint32_t)s.valid;
+  d.pad = 0;
+  return d;
+}
+
+inline uint32_t gf8_mul_host(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+  for (; b; b >>= 1) {
+    if (b & 1) r ^= a;
+    a <<= 1;
+    if (a & 0x100) a ^= 0x11D;
+  }
+  return r;
+}
+
+// v_perm tables (T0 lo, T0 hi, T1 lo, T1 hi, T2) for multiply-by-c in GF(2^8).
+inline void gf8_tables(uint32_t c, uint32_t t[5]) {
+  uint8_t b0[8], b1[8], b2[4];
+  for (int i = 0; i < 8; ++i) {
+    b0[i] = (uint8_t)gf8_mul_host(c, (uint32_t)i);
+    b1[i] = (uint8_t)gf8_mul_host(c, (uint32_t)(i << 3));
+  }
+  for (int i = 0; i < 4; ++i) b2[i] = (uint8_t)gf8_mul_host(c, (uint32_t)(i << 6));
+  auto pack = [](const uint8_t* b) {
+    return (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
+  };
+  t[0] = pack(b0);
+  t[1] = pack(b0 + 4);
+  t[2] = pack(b1);
+  t[3] = pack(b1 + 4);
+  t[4] = pack(b2);
+}
+
+template <int K, int R, bool ACC>
+int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
+  Gf8Args<K, R> a;
+  a.one = a.zero = 0;
+  uint32_t vmin = 0xFFFFFFFFu;
+  for (int j = 0; j < K; ++j) {
+    a.in[j] = dev_shard(p.in[c.j0 + j], c.o0);
+    vmin = a.in[j].valid < vmin ? a.in[j].valid : vmin;
+  }
+  for (int r = 0; r < R; ++r) {
+    a.out[r] = dev_shard(p.out[c.r0 + r], c.o0);
+    vmin = a.out[r].valid < vmin ? a.out[r].valid : vmin;
+    for (int j = 0; j < K; ++j) {
+      const uint32_t cf = p.coef[(size_t)(c.r0 + r) * p.K + c.j0 + j] & 0xFFu;
+      gf8_tables(cf, a.tab[r][j]);
+      if (cf == 1) a.one |= 1ull << (r * K + j);
+      if (cf == 0) a.zero |= 1ull << (r * K + j);
+    }
+  }
+  a.tiles = c.tiles;
+  a.vmin = vmin;
+  hipLaunchKernelGGL((gf8_apply<K, R, ACC>), dim3((uint32_t)(c.no * c.tiles)), dim3(kThreads), 0,
+                     s, a);
+  return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
+}
+
+template <int W, int R, bool ACC>
+int launch_gfw_t(const GfApply& p, const Chunk& c, hipStream_t s) {
+  GfwArgs<R> a;
+  uint32_t vmin = 0xFFFFFFFFu;
+  a.K = c.nk;
+  for (int j = 0; j < kMaxK; ++j) {
+    a.in[j] = j < c.nk ? dev_shard(p.in[c.j0 + j], c.o0) : DevShard{nullptr, 0, 0, 0};
+    if (j < c.nk) vmin = a.in[j].valid < vmin ? a.in[j].valid : vmin;
+  }
+  for (int r = 0; r < R; ++r) {
+    a.out[r] = dev_shard(p.out[c.r0 + r], c.o0);
+    vmin = a.out[r].valid < vmin ? a.out[r].valid : vmin;
+    for (int j = 0; j < kMaxK; ++j)
+      a.coef[r][j] = j < c.nk ? p.coef[(size_t)(c.r0 + r) * p.K + c.j0 + j] : 0u;
+  }
+  a.tiles = c.tiles;
+  a.vmin = vmin;
+  hipLaunchKernelGGL((gfw_apply<W, R, ACC>), dim3((uint32_t)(c.no * c.tiles)), dim3(kThreads), 0,
+                     s, a);
+  return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
+}
+
+using ChunkFn = int (*)(const GfApply&, const Chunk&, hipStream_t);
+
+// Defined (explicitly instantiated) in gf8_inst.hip, one TU per K.
+template <int K>
+ChunkFn gf8_launcher(int r, bool acc);
+
+}  // namespace detail
+}  // namespace leoec

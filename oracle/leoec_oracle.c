@@ -369,6 +369,7 @@ int orc_check_params(int coding, int k, int m, int w) {
     case ORC_VANDRS:
       if (k <= 0 || m <= 0 || w <= 0) return ORC_E_PARAMS;
       if (w != 8 && w != 16 && w != 32) return ORC_E_PARAMS_W_RS;
+      if (w == 8 && k + m > 256) return ORC_E_UNSUPPORTED; /* no Vandermonde matrix (NULL) */
       return ORC_OK;
     case ORC_CAUCHYRS:
       if (k <= 0 || m <= 0 || w <= 0) return ORC_E_PARAMS;
@@ -379,10 +380,12 @@ int orc_check_params(int coding, int k, int m, int w) {
       if (k <= 0 || m != 2 || w <= 0) return ORC_E_PARAMS_M2;
       if (k > w) return ORC_E_PARAMS_K_LE_W;
       if (w <= 2 || !(w % 2) || !is_prime(w)) return ORC_E_PARAMS_W_PRIME;
+      if (w > 32) return ORC_E_UNSUPPORTED;
       return ORC_OK;
     case ORC_ISARS:
       if (k <= 0 || m <= 0 || w <= 0) return ORC_E_PARAMS;
       if (w != 8) return ORC_E_PARAMS_W8;
+      if (k + m > 256) return ORC_E_UNSUPPORTED; /* ISA-L matrix rows are bytes */
       return ORC_OK;
     default:
       return ORC_E_INVALID_CODING;

@@ -1,0 +1,253 @@
+"""GPU parity: the HIP engine (through libleoec.so's C ABI) against the CPU
+oracle, on the reference's own test configurations (test/leo_erasure_tests.erl)
+plus the BASELINE configs.  Bit-exact everywhere (integer / byte arithmetic).
+"""
+import itertools
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+# (class, k, m, w) — suite_test_ / repair_test / parameters_test / bench_encode_test
+# configurations of test/leo_erasure_tests.erl:33-83,118-143,207-212 and BASELINE.json
+CONFIGS = [
+    ("vandrs", 10, 4, 8), ("vandrs", 4, 2, 8), ("vandrs", 8, 3, 8), ("vandrs", 6, 2, 8),
+    ("vandrs", 4, 1, 8), ("vandrs", 4, 2, 16), ("vandrs", 10, 4, 16), ("vandrs", 4, 2, 32),
+    ("vandrs", 10, 4, 32), ("vandrs", 17, 5, 8),
+    ("isars", 10, 4, 8), ("isars", 4, 2, 8), ("isars", 8, 3, 8),
+    ("cauchyrs", 4, 2, 3), ("cauchyrs", 10, 4, 8), ("cauchyrs", 10, 4, 10), ("cauchyrs", 6, 3, 4),
+    ("liberation", 4, 2, 7), ("liberation", 5, 2, 5), ("liberation", 10, 2, 11),
+    ("liberation", 4, 2, 5),
+]
+
+
+def rand_bytes(n, seed):
+    return np.random.Generator(np.random.PCG64(seed)).integers(0, 256, n, dtype=np.uint8).tobytes()
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: "%s-%d-%d-%d" % c)
+@pytest.mark.parametrize("size", [1, 1000, 65536 + 7, 300001])
+def test_encode_matches_oracle(gpu, le, oracle, cfg, size):
+    cls, k, m, w = cfg
+    data = rand_bytes(size, size * 31 + k)
+    st, blocks = le.nif_encode(cls, (k, m, w), data, size)
+    assert st == "ok", blocks
+    ref = oracle.encode(cls, k, m, w, data)
+    assert len(blocks) == k + m
+    for i, (a, b) in enumerate(zip(blocks, ref)):
+        assert a == b, f"block {i} differs"
+
+
+def _check_decode_subsets(le, cls, k, m, w, data, blocks, failures, rng, limit=None):
+    combos = list(itertools.combinations(range(k + m), k + m - failures))
+    if limit and len(combos) > limit:
+        combos = rng.sample(combos, limit)
+    for avail in combos:
+        order = list(avail)
+        rng.shuffle(order)
+        st, out = le.nif_decode(cls, (k, m, w), [blocks[i] for i in order], order, len(data))
+        assert st == "ok", (avail, out)
+        assert out == data, f"decode mismatch for survivors {avail}"
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: "%s-%d-%d-%d" % c)
+def test_decode_every_erasure_pattern(gpu, le, cfg):
+    """suite_test_: decode from every (K+M-F)-subset, shuffled, F = 0..M."""
+    cls, k, m, w = cfg
+    data = rand_bytes(40961, k * 7 + m)
+    st, blocks = le.nif_encode(cls, (k, m, w), data, len(data))
+    assert st == "ok"
+    rng = random.Random(k * 100 + m)
+    for f in range(m + 1):
+        _check_decode_subsets(le, cls, k, m, w, data, blocks, f, rng, limit=300)
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: "%s-%d-%d-%d" % c)
+def test_repair_every_pair(gpu, le, cfg):
+    """repair_test: every 2-erasure pair repaired equals the encoded blocks."""
+    cls, k, m, w = cfg
+    data = rand_bytes(33333, k + 5 * m)
+    st, blocks = le.nif_encode(cls, (k, m, w), data, len(data))
+    assert st == "ok"
+    full = list(range(k + m))
+    for lost in itertools.combinations(full, min(2, m)):
+        avail = [i for i in full if i not in lost]
+        st, rep = le.nif_repair(cls, (k, m, w), [blocks[i] for i in avail], avail, list(lost))
+        assert st == "ok", rep
+        assert rep == [blocks[i] for i in lost], f"repair of {lost} differs"
+
+
+def test_repair_matches_oracle_with_extra_survivors(gpu, le, oracle):
+    """More than k survivors, in arbitrary order: same survivor choice as the
+    reference (first k intact ids ascending; isars: first k listed)."""
+    for cls, k, m, w in [("vandrs", 10, 4, 8), ("isars", 10, 4, 8), ("cauchyrs", 10, 4, 8),
+                         ("liberation", 4, 2, 7)]:
+        data = rand_bytes(20000, 5)
+        blocks = oracle.encode(cls, k, m, w, data)
+        ids = [13 % (k + m), 2, 0, 7 % (k + m), 1, 5, 3, 4, 8 % (k + m), 9 % (k + m), 11 % (k + m)]
+        ids = list(dict.fromkeys(ids))[: k + 1]
+        lost = [i for i in range(k + m) if i not in ids]
+        # corrupt-free: the map is unique, so also compare against the oracle
+        st, rep = le.nif_repair(cls, (k, m, w), [blocks[i] for i in ids], ids, lost)
+        assert st == "ok"
+        assert rep == oracle.repair(cls, k, m, w, [blocks[i] for i in ids], ids, lost)
+
+
+def test_padding_10MiB_plus_1(gpu, le, oracle):
+    """TEST_SIZE = 10485760 + 1 (test/leo_erasure_tests.erl:28)."""
+    data = rand_bytes(10485760 + 1, 28)
+    for cls, k, m, w in [("vandrs", 10, 4, 8), ("isars", 10, 4, 8), ("cauchyrs", 4, 2, 3),
+                         ("liberation", 4, 2, 7)]:
+        st, blocks = le.nif_encode(cls, (k, m, w), data, len(data))
+        assert st == "ok"
+        assert blocks == oracle.encode(cls, k, m, w, data)
+        rng = random.Random(1)
+        _check_decode_subsets(le, cls, k, m, w, data, blocks, m, rng, limit=6)
+
+
+@pytest.mark.parametrize("km", [(10, 4), (8, 3), (6, 2), (4, 2), (4, 1)])
+def test_correctness_5MiB(gpu, le, km):
+    """correctness_test (test/leo_erasure_tests.erl:171-204), default coder."""
+    k, m = km
+    data = rand_bytes(5 * 1024 * 1024, k * m)
+    st, id_blocks = le.encode((k, m), data)
+    assert st == "ok" and len(id_blocks) == k + m
+    st, out = le.decode((k, m), id_blocks, len(data))
+    assert st == "ok" and out == data
+    lost = (k * 7 + m) % (k + m)
+    rest = [x for x in id_blocks if x[0] != lost]
+    st, rep = le.repair((k, m), rest)
+    assert st == "ok" and rep == [id_blocks[lost]]
+
+
+def test_parameters(gpu, le):
+    """parameters_test (test/leo_erasure_tests.erl:214-275)."""
+    data = rand_bytes(1024, 3)
+    assert le.encode("vandrs", (4, 2, 7), data)[0] == "error"
+    for cls, p in [("vandrs", (4, 2, 8)), ("cauchyrs", (4, 2, 3)), ("liberation", (4, 2, 5)),
+                   ("isars", (4, 2, 8))]:
+        st, idb = le.encode(cls, p, data)
+        assert st == "ok"
+        blocks = [b for _, b in idb]
+        assert le.decode(cls, p, blocks, [0, 1, 2], len(data))[0] == "error"
+        # genuinely too few blocks (3 blocks with 3 ids)
+        assert le.decode(cls, p, blocks[:3], [0, 1, 2], len(data)) == \
+            ("error", "Not Enough Blocks")
+        assert le.decode(cls, p, blocks[:4] + blocks[:1], [0, 1, 2, 3, 0], len(data)) == \
+            ("error", "Blocks should be unique")
+    assert le.encode("cauchyrs", (10, 4, 3), data)[0] == "error"
+    assert le.encode("liberation", (4, 2, 6), data)[0] == "error"
+    assert le.encode("liberation", (4, 2, 3), data)[0] == "error"
+    assert le.encode("isars", (4, 2, 7), data)[0] == "error"
+    assert le.encode("unkown", (4, 2, 3), data) == ("error", "Invalid Coding")
+    assert le.encode("liberation", ("troll",), data)[0] == "error"
+    assert le.encode((4, 2, 5), "liberation", data)[0] == "error"
+    for km, n in [((10, 4), 14), ((8, 3), 11), ((6, 2), 8)]:
+        st, idb = le.encode(km, data)
+        assert st == "ok" and len(idb) == n
+        assert le.decode(km, idb, len(data)) == ("ok", data)
+
+
+def test_edge_sizes(gpu, le, oracle):
+    """Empty and ragged objects; trailing data blocks that are pure padding
+    (the reference's fast-path overflow case, rscoding.cpp:116-120)."""
+    for size in [0, 1, 15, 16, 17, 127, 128, 129, 1024, 1279, 1281]:
+        data = rand_bytes(size, size + 1)
+        for cls, k, m, w in [("vandrs", 10, 4, 8), ("cauchyrs", 10, 4, 8), ("isars", 4, 2, 8)]:
+            st, blocks = le.nif_encode(cls, (k, m, w), data, size)
+            assert st == "ok"
+            assert blocks == oracle.encode(cls, k, m, w, data)
+            ids = list(range(k))
+            st, out = le.nif_decode(cls, (k, m, w), [blocks[i] for i in ids], ids, size)
+            assert st == "ok" and out == data
+            ids = list(range(m, k + m))
+            st, out = le.nif_decode(cls, (k, m, w), [blocks[i] for i in ids], ids, size)
+            assert st == "ok" and out == data
+
+
+# ---------------------------------------------------------------------------
+# device-resident batched API
+def _batch(gpu, n, size, stride, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    host = rng.integers(0, 256, (n, stride), dtype=np.uint8)
+    return host, gpu.from_numpy(host).cuda()
+
+
+@pytest.mark.parametrize("cfg", [("vandrs", 10, 4, 8), ("vandrs", 4, 2, 8), ("isars", 10, 4, 8),
+                                 ("cauchyrs", 10, 4, 8), ("liberation", 4, 2, 7),
+                                 ("vandrs", 10, 4, 16), ("vandrs", 6, 3, 32)],
+                         ids=lambda c: "%s-%d-%d-%d" % c)
+def test_device_encode_batch(gpu, le, oracle, cfg):
+    cls, k, m, w = cfg
+    n, size = 24, 200003
+    bs, _ = le.layout(cls, (k, m, w), size)
+    host, objs = _batch(gpu, n, size, size + 62, 11)  # stride not a multiple of 16 -> rejected
+    parity = gpu.empty((n, m * bs), dtype=gpu.uint8, device="cuda")
+    with pytest.raises(le.LeoecError):
+        le.device.encode(cls, (k, m, w), objs, size, parity)
+    host, objs = _batch(gpu, n, size, size + 77 - (size + 77) % 16, 12)
+    le.device.encode(cls, (k, m, w), objs, size, parity)
+    gpu.cuda.synchronize()
+    par = parity.cpu().numpy()
+    for o in range(n):
+        ref = oracle.encode(cls, k, m, w, host[o, :size].tobytes())
+        assert par[o].tobytes() == b"".join(ref[k:]), f"object {o}"
+
+
+def test_device_decode_all_1001_patterns(gpu, le):
+    """vandrs RS(10,4,8): every 4-erasure pattern, rebuilt in place."""
+    k, m, w = 10, 4, 8
+    n, size = 8, 1048576
+    bs, _ = le.layout("vandrs", (k, m, w), size)
+    host, objs = _batch(gpu, n, size, size, 99)
+    parity = gpu.empty((n, m * bs), dtype=gpu.uint8, device="cuda")
+    le.device.encode("vandrs", (k, m, w), objs, size, parity)
+    ref = objs.clone()
+    work = objs.clone()
+    for erased in itertools.combinations(range(k + m), m):
+        work.copy_(ref)
+        for e in erased:
+            if e < k:
+                lo, hi = e * bs, min((e + 1) * bs, size)
+                work[:, lo:hi] = 0xA5
+        le.device.decode("vandrs", (k, m, w), work, size, parity, list(erased))
+        if not gpu.equal(work, ref):
+            raise AssertionError(f"in-place decode wrong for erasures {erased}")
+
+
+def test_device_repair(gpu, le, oracle):
+    for cls, k, m, w in [("vandrs", 10, 4, 8), ("cauchyrs", 10, 4, 8), ("isars", 10, 4, 8)]:
+        n, size = 16, 123457
+        bs, _ = le.layout(cls, (k, m, w), size)
+        host = np.random.Generator(np.random.PCG64(3)).integers(0, 256, (n, size), dtype=np.uint8)
+        blocks = np.zeros((k + m, n, bs), dtype=np.uint8)
+        for o in range(n):
+            ref = oracle.encode(cls, k, m, w, host[o].tobytes())
+            for b in range(k + m):
+                blocks[b, o] = np.frombuffer(ref[b], dtype=np.uint8)
+        dev = [gpu.from_numpy(blocks[b]).cuda() for b in range(k + m)]
+        lost = [0, 5, 10, 13]
+        avail = [None if b in lost else dev[b] for b in range(k + m)]
+        out = [gpu.empty((n, bs), dtype=gpu.uint8, device="cuda") for _ in lost]
+        le.device.repair(cls, (k, m, w), avail, bs, lost, out, n)
+        gpu.cuda.synchronize()
+        for r, b in enumerate(lost):
+            assert np.array_equal(out[r].cpu().numpy(), blocks[b]), (cls, b)
+
+
+def test_device_roundtrip_bench_shape(gpu, le):
+    """Size-independent property at the bench configuration: 1 MiB objects,
+    RS(10,4,8), encode then in-place decode of {0,1,2,3} restores every byte."""
+    k, m, w = 10, 4, 8
+    n, size = 256, 1048576
+    bs, _ = le.layout("vandrs", (k, m, w), size)
+    g = gpu.Generator(device="cuda").manual_seed(0x1E0E)
+    objs = gpu.randint(0, 256, (n, size), dtype=gpu.uint8, device="cuda", generator=g)
+    parity = gpu.empty((n, m * bs), dtype=gpu.uint8, device="cuda")
+    le.device.encode("vandrs", (k, m, w), objs, size, parity)
+    ref = objs.clone()
+    objs[:, : 4 * bs] = 0
+    le.device.decode("vandrs", (k, m, w), objs, size, parity, [0, 1, 2, 3])
+    assert gpu.equal(objs, ref)
