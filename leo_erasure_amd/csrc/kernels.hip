@@ -1,6 +1,7 @@
 // kernels.hip — dispatch of GfApply / BitApply plans onto the gfx950 kernels
 // of kernels_impl.hpp (w = 16/32 and bitmatrix instances live here; GF(2^8)
 // instances in gf8_inst.hip).
+#include <cstdlib>
 #include <utility>
 
 #include "kernels_impl.hpp"
@@ -33,6 +34,13 @@ ChunkFn gfw_pick(int r, bool acc) {
   return tbl[acc ? 1 : 0][r - 1];
 }
 
+// LEOEC_GF8_VARIANT=<n> selects a measurement variant of gf8_apply<10,4>
+// (tools/kvariants.py); unset or 0 = the shipped kernel.
+int gf8_variant_env() {
+  const char* e = std::getenv("LEOEC_GF8_VARIANT");
+  return e ? std::atoi(e) : 0;
+}
+
 }  // namespace
 
 int launch(const GfApply& p, hipStream_t s) {
@@ -54,12 +62,17 @@ int launch(const GfApply& p, hipStream_t s) {
         const int nk = (p.K - j0 < kMaxK) ? p.K - j0 : kMaxK;
         const Chunk c{r0, nr, j0, nk, o0, no, tiles};
         ChunkFn fn;
-        if (p.w == 8)
+        if (p.w == 8) {
           fn = gf8_pick(std::make_index_sequence<kMaxK>{}, nk, nr, j0 > 0);
-        else if (p.w == 16)
+          if (nk == 10 && nr == 4 && j0 == 0) {
+            const int var = gf8_variant_env();
+            if (var > 0 && gf8_variant(var)) fn = gf8_variant(var);
+          }
+        } else if (p.w == 16) {
           fn = gfw_pick<16>(nr, j0 > 0);
-        else
+        } else {
           fn = gfw_pick<32>(nr, j0 > 0);
+        }
         const int rc = fn(p, c, s);
         if (rc) return rc;
       }

@@ -66,6 +66,19 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
+// 16-byte global access; NT = non-temporal (data streamed once: measured
+// +9 % on the RS(10,4) encode, tools/kvariants.py).
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
+  if (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return *reinterpret_cast<const u32x4*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
+  if (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  else *reinterpret_cast<u32x4*>(p) = v;
+}
+
 // Bytes of v at index >= n (0 <= n < 16) cleared.
 __device__ __forceinline__ u32x4 keep_first(u32x4 v, uint32_t n) {
 #pragma unroll
@@ -82,7 +95,7 @@ __device__ __forceinline__ u32x4 keep_first(u32x4 v, uint32_t n) {
 // page) and its bytes past `valid` cleared; chunks past `valid` are not read.
 __device__ __forceinline__ u32x4 load_guarded(const uint8_t* p, uint32_t off, uint32_t valid) {
   u32x4 v = {0u, 0u, 0u, 0u};
-  if (off < valid) v = *reinterpret_cast<const u32x4*>(p + off);
+  if (off < valid) v = ld16<true>(p + off);
   if (off + 16u > valid) v = keep_first(v, off < valid ? valid - off : 0u);
   return v;
 }
@@ -90,7 +103,7 @@ __device__ __forceinline__ u32x4 load_guarded(const uint8_t* p, uint32_t off, ui
 // Guarded store: never writes a byte at or past `valid`.
 __device__ __forceinline__ void store_guarded(uint8_t* p, uint32_t off, uint32_t valid, u32x4 v) {
   if (off + 16u <= valid) {
-    *reinterpret_cast<u32x4*>(p + off) = v;
+    st16<true>(p + off, v);
   } else if (off < valid) {
     const uint32_t n = valid - off;
 #pragma unroll
@@ -112,70 +125,107 @@ struct Gf8Args {
   uint32_t vmin;          // min valid over all shards of the launch
 };
 
-template <int K, int R, bool ACC>
+// Kernel shape / policy knobs (the engine ships kGf8Default; the others exist
+// for A/B measurement through LEOEC_GF8_VARIANT, see tools/kvariants.py).
+struct Gf8Opt {
+  int cpt;       // 16-byte columns per lane (tile = 4 KiB * cpt per block)
+  bool nt;       // non-temporal loads / stores (streamed once, never re-read)
+  bool branchy;  // scalar branch on coefficients 0 / 1 instead of table lookups
+  bool copy;     // measurement only: same traffic, XOR instead of GF multiply
+};
+constexpr Gf8Opt kGf8Default{1, true, true, false};
+
+
+template <int K, int R, bool ACC, int CPT, bool NT, bool BRANCHY, bool COPY>
 __global__ void __launch_bounds__(kThreads) gf8_apply(const Gf8Args<K, R> a) {
+  constexpr uint32_t TB = kTileBytes * CPT;
   const uint32_t obj = blockIdx.x / a.tiles;
   const uint32_t tile = blockIdx.x - obj * a.tiles;
-  const uint32_t t0 = tile * kTileBytes;
+  const uint32_t t0 = tile * TB;
   const uint32_t off = t0 + threadIdx.x * 16u;
-  const bool full = t0 + kTileBytes <= a.vmin;  // wave-uniform
+  const bool full = t0 + TB <= a.vmin;  // wave-uniform
   const uint64_t o = obj;
 
-  u32x4 d[K];
+  u32x4 d[CPT][K];
   if (full) {
 #pragma unroll
     for (int j = 0; j < K; ++j)
-      d[j] = *reinterpret_cast<const u32x4*>(a.in[j].base + o * a.in[j].stride + off);
+#pragma unroll
+      for (int c = 0; c < CPT; ++c)
+        d[c][j] = ld16<NT>(a.in[j].base + o * a.in[j].stride + off + c * kTileBytes);
   } else {
 #pragma unroll
     for (int j = 0; j < K; ++j)
-      d[j] = load_guarded(a.in[j].base + o * a.in[j].stride, off, a.in[j].valid);
-  }
-  u32x4 acc[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    acc[r] = u32x4{0u, 0u, 0u, 0u};
-    if (ACC) acc[r] = load_guarded(a.out[r].base + o * a.out[r].stride, off, a.out[r].valid);
+      for (int c = 0; c < CPT; ++c)
+        d[c][j] = load_guarded(a.in[j].base + o * a.in[j].stride, off + c * kTileBytes,
+                               a.in[j].valid);
   }
+  u32x4 acc[CPT][R];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      acc[c][r] = u32x4{0u, 0u, 0u, 0u};
+      if (ACC)
+        acc[c][r] = load_guarded(a.out[r].base + o * a.out[r].stride, off + c * kTileBytes,
+                                 a.out[r].valid);
+    }
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    uint32_t s0[4], s1[4], s2[4];
+    if (COPY) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const uint32_t x = d[j][e];
-      s0[e] = x & 0x07070707u;
-      s1[e] = (x >> 3) & 0x07070707u;
-      s2[e] = (x >> 6) & 0x03030303u;
+      for (int c = 0; c < CPT; ++c)
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[c][r] ^= d[c][j];
+      continue;
     }
+    uint32_t s0[CPT][4], s1[CPT][4], s2[CPT][4];
+#pragma unroll
+    for (int c = 0; c < CPT; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t x = d[c][j][e];
+        s0[c][e] = x & 0x07070707u;
+        s1[c][e] = (x >> 3) & 0x07070707u;
+        s2[c][e] = (x >> 6) & 0x03030303u;
+      }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int bit = r * K + j;
-      if ((a.one >> bit) & 1) {
-        acc[r] ^= d[j];
-      } else if (!((a.zero >> bit) & 1)) {
+      if (BRANCHY && ((a.one >> bit) & 1)) {
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) acc[c][r] ^= d[c][j];
+      } else if (!BRANCHY || !((a.zero >> bit) & 1)) {
         const uint32_t t0l = a.tab[r][j][0], t0h = a.tab[r][j][1];
         const uint32_t t1l = a.tab[r][j][2], t1h = a.tab[r][j][3];
         const uint32_t t2 = a.tab[r][j][4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t p0 = perm(t0h, t0l, s0[e]);
-          const uint32_t p1 = perm(t1h, t1l, s1[e]);
-          const uint32_t p2 = perm(t2, t2, s2[e]);
-          acc[r][e] = xor3(acc[r][e], p0, p1) ^ p2;
-        }
+        for (int c = 0; c < CPT; ++c)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t p0 = perm(t0h, t0l, s0[c][e]);
+            const uint32_t p1 = perm(t1h, t1l, s1[c][e]);
+            const uint32_t p2 = perm(t2, t2, s2[c][e]);
+            acc[c][r][e] = xor3(acc[c][r][e], p0, p1) ^ p2;
+          }
       }
     }
   }
   if (full) {
 #pragma unroll
     for (int r = 0; r < R; ++r)
-      *reinterpret_cast<u32x4*>(const_cast<uint8_t*>(a.out[r].base) + o * a.out[r].stride + off) =
-          acc[r];
+#pragma unroll
+      for (int c = 0; c < CPT; ++c)
+        st16<NT>(const_cast<uint8_t*>(a.out[r].base) + o * a.out[r].stride + off + c * kTileBytes,
+                 acc[c][r]);
   } else {
 #pragma unroll
     for (int r = 0; r < R; ++r)
-      store_guarded(const_cast<uint8_t*>(a.out[r].base) + o * a.out[r].stride, off,
-                    a.out[r].valid, acc[r]);
+#pragma unroll
+      for (int c = 0; c < CPT; ++c)
+        store_guarded(const_cast<uint8_t*>(a.out[r].base) + o * a.out[r].stride,
+                      off + c * kTileBytes, a.out[r].valid, acc[c][r]);
   }
 }
 
@@ -222,7 +272,7 @@ __global__ void __launch_bounds__(kThreads) gfw_apply(const GfwArgs<R> a) {
   }
   for (int j = 0; j < a.K; ++j) {
     const uint8_t* p = a.in[j].base + o * a.in[j].stride;
-    u32x4 x = full ? *reinterpret_cast<const u32x4*>(p + off) : load_guarded(p, off, a.in[j].valid);
+    u32x4 x = full ? ld16<true>(p + off) : load_guarded(p, off, a.in[j].valid);
     uint32_t c[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) c[r] = a.coef[r][j];
@@ -335,7 +385,8 @@ inline void gf8_tables(uint32_t c, uint32_t t[5]) {
   t[4] = pack(b2);
 }
 
-template <int K, int R, bool ACC>
+template <int K, int R, bool ACC, int CPT = kGf8Default.cpt, bool NT = kGf8Default.nt,
+          bool BRANCHY = kGf8Default.branchy, bool COPY = kGf8Default.copy>
 int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   Gf8Args<K, R> a;
   a.one = a.zero = 0;
@@ -354,10 +405,11 @@ int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
       if (cf == 0) a.zero |= 1ull << (r * K + j);
     }
   }
-  a.tiles = c.tiles;
+  const uint32_t tb = kTileBytes * CPT;
+  a.tiles = (uint32_t)((p.block_size + tb - 1) / tb);
   a.vmin = vmin;
-  hipLaunchKernelGGL((gf8_apply<K, R, ACC>), dim3((uint32_t)(c.no * c.tiles)), dim3(kThreads), 0,
-                     s, a);
+  hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, BRANCHY, COPY>),
+                     dim3((uint32_t)(c.no * a.tiles)), dim3(kThreads), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }
 
@@ -388,6 +440,9 @@ using ChunkFn = int (*)(const GfApply&, const Chunk&, hipStream_t);
 // Defined (explicitly instantiated) in gf8_inst.hip, one TU per K.
 template <int K>
 ChunkFn gf8_launcher(int r, bool acc);
+
+// Measurement variants of gf8_apply<10, 4> (gf8_exp.hip); nullptr if unknown.
+ChunkFn gf8_variant(int variant);
 
 }  // namespace detail
 }  // namespace leoec
