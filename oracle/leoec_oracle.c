@@ -800,7 +800,9 @@ static void *bench_worker(void *arg) {
     } else {
       nin = k;
       for (int j = 0; j < k; j++) in[j] = J->surv[j] < k ? blk[J->surv[j]] : par + (uint64_t)(J->surv[j] - k) * bs;
-      for (int i = 0; i < J->nout; i++) out[i] = dec + (uint64_t)i * bs;
+      /* in place, as the GPU decode: the rebuilt data blocks overwrite their
+       * own (identical) bytes in the object / staged tail */
+      for (int i = 0; i < J->nout; i++) out[i] = (uint8_t *)blk[J->want[i]];
     }
 #if defined(__x86_64__)
     if (J->simd >= 2) apply_avx2(nin, J->nout, J->tbl, in, out, bs);

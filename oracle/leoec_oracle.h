@@ -19,6 +19,13 @@
  *      c_src/cauchycoding.cpp:29-213, c_src/liberationcoding.cpp:29-208,
  *      c_src/irscoding.cpp:32-220).
  * Pins: see tests/test_oracle.py (KATs) and DESIGN.md §Oracle.
+ *
+ * PARITY UNPINNED (strict sense): the reference's tests hold no known-answer
+ * vectors and the reference cannot be built or run here (no Erlang/OTP, its
+ * Jerasure / gf-complete / ISA-L dependencies are absent), so no vector in
+ * tests/ comes from the reference itself.  The restatement is pinned by
+ * recalled public KATs (Jerasure manual reed_sol_01 7 7 8, cbest_2..5), an
+ * independent numpy restatement, and the reference's round-trip properties.
  */
 #ifndef LEOEC_ORACLE_H
 #define LEOEC_ORACLE_H

@@ -196,3 +196,9 @@ def test_cpu_baseline_matches_oracle(oracle):
         for o in range(n):
             ref = oracle.encode("vandrs", k, m, 8, objs[o].tobytes())
             assert par[o].tobytes() == b"".join(ref[k:])
+        # in-place decode of data blocks {0,1,2,3} rebuilds the same bytes
+        work = objs.copy()
+        work[:, :4 * bs] = 0
+        oracle.bench_rs8(1, k, m, work, size, size, n, par, erased=[0, 1, 2, 3], threads=2,
+                         force_scalar=force_scalar)
+        assert np.array_equal(work, objs)
