@@ -7,20 +7,16 @@ namespace leoec {
 namespace detail {
 
 ChunkFn gf8_variant(int v) {
-  //                            K   R  ACC    CPT  NT     BRANCHY COPY
+  //                            K   R  ACC    CPT  NT     BRANCHY COPY   PIPE
   switch (v) {
-    case 1: return &launch_gf8_t<10, 4, false, 1, true, true, false>;   // shipped
-    case 11: return &launch_gf8_t<10, 4, false, 1, true, false, false>;  // nt + branchfree
-    case 12: return &launch_gf8_t<10, 4, false, 1, false, true, false>;  // no nt
-    case 2: return &launch_gf8_t<10, 4, false, 2, false, true, false>;
-    case 3: return &launch_gf8_t<10, 4, false, 1, true, true, false>;
-    case 4: return &launch_gf8_t<10, 4, false, 2, true, true, false>;
-    case 5: return &launch_gf8_t<10, 4, false, 1, false, false, false>;
-    case 6: return &launch_gf8_t<10, 4, false, 1, false, true, true>;
-    case 7: return &launch_gf8_t<10, 4, false, 1, true, true, true>;
-    case 8: return &launch_gf8_t<10, 4, false, 2, false, false, false>;
-    case 9: return &launch_gf8_t<10, 4, false, 4, false, true, false>;
-    case 10: return &launch_gf8_t<10, 4, false, 2, false, true, true>;
+    case 1: return &launch_gf8_t<10, 4, false, 1, true, -1, false, false>;  // shipped
+    case 2: return &launch_gf8_t<10, 4, false, 2, true, -1, false, false>;
+    case 3: return &launch_gf8_t<10, 4, false, 1, true, 1, false, false>;   // always branchy
+    case 5: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false>;   // always paired
+    case 7: return &launch_gf8_t<10, 4, false, 1, true, 1, true, false>;    // copy-xor
+    case 12: return &launch_gf8_t<10, 4, false, 1, false, -1, false, false>;  // no nt
+    case 13: return &launch_gf8_t<10, 4, false, 1, true, -1, false, true>;  // persistent prefetch
+    case 14: return &launch_gf8_t<10, 4, false, 1, true, 1, true, true>;    // copy-xor persistent
     default: return nullptr;
   }
 }

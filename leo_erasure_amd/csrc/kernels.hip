@@ -43,6 +43,19 @@ int gf8_variant_env() {
 
 }  // namespace
 
+namespace detail {
+int device_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      return 256;
+    return n;
+  }();
+  return cus;
+}
+}  // namespace detail
+
 int launch(const GfApply& p, hipStream_t s) {
   if (p.K <= 0 || p.R <= 0 || (int)p.in.size() != p.K || (int)p.out.size() != p.R ||
       p.coef.size() != (size_t)p.K * p.R)

@@ -123,6 +123,7 @@ struct Gf8Args {
   uint64_t zero;          // bit r*K+j set: coefficient is 0
   uint32_t tiles;         // tiles per object
   uint32_t vmin;          // min valid over all shards of the launch
+  uint32_t total_tiles;   // tiles of the launch (persistent form)
 };
 
 // Kernel shape / policy knobs (the engine ships kGf8Default; the others exist
@@ -136,41 +137,15 @@ struct Gf8Opt {
 constexpr Gf8Opt kGf8Default{1, true, true, false};
 
 
-template <int K, int R, bool ACC, int CPT, bool NT, bool BRANCHY, bool COPY>
-__global__ void __launch_bounds__(kThreads) gf8_apply(const Gf8Args<K, R> a) {
-  constexpr uint32_t TB = kTileBytes * CPT;
-  const uint32_t obj = blockIdx.x / a.tiles;
-  const uint32_t tile = blockIdx.x - obj * a.tiles;
-  const uint32_t t0 = tile * TB;
-  const uint32_t off = t0 + threadIdx.x * 16u;
-  const bool full = t0 + TB <= a.vmin;  // wave-uniform
-  const uint64_t o = obj;
-
-  u32x4 d[CPT][K];
-  if (full) {
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-#pragma unroll
-      for (int c = 0; c < CPT; ++c)
-        d[c][j] = ld16<NT>(a.in[j].base + o * a.in[j].stride + off + c * kTileBytes);
-  } else {
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-#pragma unroll
-      for (int c = 0; c < CPT; ++c)
-        d[c][j] = load_guarded(a.in[j].base + o * a.in[j].stride, off + c * kTileBytes,
-                               a.in[j].valid);
-  }
-  u32x4 acc[CPT][R];
-#pragma unroll
-  for (int c = 0; c < CPT; ++c)
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      acc[c][r] = u32x4{0u, 0u, 0u, 0u};
-      if (ACC)
-        acc[c][r] = load_guarded(a.out[r].base + o * a.out[r].stride, off + c * kTileBytes,
-                                 a.out[r].valid);
-    }
+// One tile of the GF(2^8) map for columns already loaded in d.
+//  BRANCHY: coefficient 1 -> plain xor, 0 -> skip (scalar branches), others
+//           3 perm + xor3 + xor;
+//  !BRANCHY: every coefficient through its tables, with the 3K perm outputs
+//           of a row folded pairwise by xor3 (1.5 ops per coefficient).
+template <int K, int R, int CPT, bool BRANCHY, bool COPY>
+__device__ __forceinline__ void gf8_tile(const Gf8Args<K, R>& a, const u32x4 (&d)[CPT][K],
+                                         u32x4 (&acc)[CPT][R]) {
+  u32x4 pend[CPT][R];
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     if (COPY) {
@@ -207,11 +182,63 @@ __global__ void __launch_bounds__(kThreads) gf8_apply(const Gf8Args<K, R> a) {
             const uint32_t p0 = perm(t0h, t0l, s0[c][e]);
             const uint32_t p1 = perm(t1h, t1l, s1[c][e]);
             const uint32_t p2 = perm(t2, t2, s2[c][e]);
-            acc[c][r][e] = xor3(acc[c][r][e], p0, p1) ^ p2;
+            if (BRANCHY) {
+              acc[c][r][e] = xor3(acc[c][r][e], p0, p1) ^ p2;
+            } else if ((j & 1) == 0) {  // static after unrolling
+              acc[c][r][e] = xor3(acc[c][r][e], p0, p1);
+              pend[c][r][e] = p2;
+            } else {
+              acc[c][r][e] = xor3(acc[c][r][e], pend[c][r][e], p0);
+              acc[c][r][e] = xor3(acc[c][r][e], p1, p2);
+            }
           }
       }
     }
   }
+  if (!BRANCHY && !COPY && (K & 1)) {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c)
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[c][r] ^= pend[c][r];
+  }
+}
+
+template <int K, int R, int CPT, bool NT>
+__device__ __forceinline__ void gf8_load(const Gf8Args<K, R>& a, uint64_t o, uint32_t off,
+                                         bool full, u32x4 (&d)[CPT][K]) {
+  if (full) {
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+      for (int c = 0; c < CPT; ++c)
+        d[c][j] = ld16<NT>(a.in[j].base + o * a.in[j].stride + off + c * kTileBytes);
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+      for (int c = 0; c < CPT; ++c)
+        d[c][j] = load_guarded(a.in[j].base + o * a.in[j].stride, off + c * kTileBytes,
+                               a.in[j].valid);
+  }
+}
+
+template <int K, int R, bool ACC, int CPT, bool NT>
+__device__ __forceinline__ void gf8_init_store(const Gf8Args<K, R>& a, uint64_t o, uint32_t off,
+                                               u32x4 (&acc)[CPT][R]) {
+#pragma unroll
+  for (int c = 0; c < CPT; ++c)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      acc[c][r] = u32x4{0u, 0u, 0u, 0u};
+      if (ACC)
+        acc[c][r] = load_guarded(a.out[r].base + o * a.out[r].stride, off + c * kTileBytes,
+                                 a.out[r].valid);
+    }
+}
+
+template <int K, int R, int CPT, bool NT>
+__device__ __forceinline__ void gf8_store(const Gf8Args<K, R>& a, uint64_t o, uint32_t off,
+                                          bool full, const u32x4 (&acc)[CPT][R]) {
   if (full) {
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -226,6 +253,58 @@ __global__ void __launch_bounds__(kThreads) gf8_apply(const Gf8Args<K, R> a) {
       for (int c = 0; c < CPT; ++c)
         store_guarded(const_cast<uint8_t*>(a.out[r].base) + o * a.out[r].stride,
                       off + c * kTileBytes, a.out[r].valid, acc[c][r]);
+  }
+}
+
+// One workgroup per tile (PIPE = false), or a persistent grid that walks the
+// tiles and issues the loads of its next tile before computing the current
+// one (PIPE = true).
+template <int K, int R, bool ACC, int CPT, bool NT, bool BRANCHY, bool COPY, bool PIPE>
+__global__ void __launch_bounds__(kThreads) gf8_apply(const Gf8Args<K, R> a) {
+  constexpr uint32_t TB = kTileBytes * CPT;
+  if (!PIPE) {
+    const uint32_t obj = blockIdx.x / a.tiles;
+    const uint32_t tile = blockIdx.x - obj * a.tiles;
+    const uint32_t t0 = tile * TB;
+    const uint32_t off = t0 + threadIdx.x * 16u;
+    const bool full = t0 + TB <= a.vmin;  // wave-uniform
+    u32x4 d[CPT][K];
+    gf8_load<K, R, CPT, NT>(a, obj, off, full, d);
+    u32x4 acc[CPT][R];
+    gf8_init_store<K, R, ACC, CPT, NT>(a, obj, off, acc);
+    gf8_tile<K, R, CPT, BRANCHY, COPY>(a, d, acc);
+    gf8_store<K, R, CPT, NT>(a, obj, off, full, acc);
+    return;
+  }
+  const uint32_t total = a.total_tiles;
+  uint32_t g = blockIdx.x;
+  if (g >= total) return;
+  u32x4 nxt[CPT][K];
+  uint32_t obj = g / a.tiles;
+  uint32_t t0 = (g - obj * a.tiles) * TB;
+  bool full = t0 + TB <= a.vmin;
+  gf8_load<K, R, CPT, NT>(a, obj, t0 + threadIdx.x * 16u, full, nxt);
+  while (true) {
+    u32x4 d[CPT][K];
+#pragma unroll
+    for (int c = 0; c < CPT; ++c)
+#pragma unroll
+      for (int j = 0; j < K; ++j) d[c][j] = nxt[c][j];
+    const uint32_t cobj = obj, coff = t0 + threadIdx.x * 16u;
+    const bool cfull = full;
+    g += gridDim.x;
+    const bool more = g < total;
+    if (more) {
+      obj = g / a.tiles;
+      t0 = (g - obj * a.tiles) * TB;
+      full = t0 + TB <= a.vmin;
+      gf8_load<K, R, CPT, NT>(a, obj, t0 + threadIdx.x * 16u, full, nxt);
+    }
+    u32x4 acc[CPT][R];
+    gf8_init_store<K, R, ACC, CPT, NT>(a, cobj, coff, acc);
+    gf8_tile<K, R, CPT, BRANCHY, COPY>(a, d, acc);
+    gf8_store<K, R, CPT, NT>(a, cobj, coff, cfull, acc);
+    if (!more) break;
   }
 }
 
@@ -385,12 +464,17 @@ inline void gf8_tables(uint32_t c, uint32_t t[5]) {
   t[4] = pack(b2);
 }
 
+int device_cus();  // compute units of the current device (kernels.hip)
+
+// BRANCHY = -1: pick per launch from the coefficients (scalar-branch form
+// when enough coefficients are 0/1, the paired all-table form otherwise).
 template <int K, int R, bool ACC, int CPT = kGf8Default.cpt, bool NT = kGf8Default.nt,
-          bool BRANCHY = kGf8Default.branchy, bool COPY = kGf8Default.copy>
+          int BRANCHY = -1, bool COPY = kGf8Default.copy, bool PIPE = false>
 int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   Gf8Args<K, R> a;
   a.one = a.zero = 0;
   uint32_t vmin = 0xFFFFFFFFu;
+  int n01 = 0;
   for (int j = 0; j < K; ++j) {
     a.in[j] = dev_shard(p.in[c.j0 + j], c.o0);
     vmin = a.in[j].valid < vmin ? a.in[j].valid : vmin;
@@ -403,13 +487,28 @@ int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
       gf8_tables(cf, a.tab[r][j]);
       if (cf == 1) a.one |= 1ull << (r * K + j);
       if (cf == 0) a.zero |= 1ull << (r * K + j);
+      n01 += cf <= 1;
     }
   }
   const uint32_t tb = kTileBytes * CPT;
   a.tiles = (uint32_t)((p.block_size + tb - 1) / tb);
   a.vmin = vmin;
-  hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, BRANCHY, COPY>),
-                     dim3((uint32_t)(c.no * a.tiles)), dim3(kThreads), 0, s, a);
+  a.total_tiles = (uint32_t)(c.no * a.tiles);
+  // per-dword VALU: general coefficient 5.5 (branchy) vs 5 (paired); a 1 costs
+  // 1 and a 0 nothing in the branchy form
+  const int n = R * K;
+  const bool branchy = BRANCHY >= 0 ? BRANCHY != 0 : (11 * (n - n01) + 2 * n01 < 10 * n);
+  uint32_t grid = a.total_tiles;
+  if (PIPE) {
+    const uint32_t cap = (uint32_t)device_cus() * 4u;
+    grid = grid < cap ? grid : cap;
+  }
+  if (branchy)
+    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, true, COPY, PIPE>), dim3(grid),
+                       dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, false, COPY, PIPE>), dim3(grid),
+                       dim3(kThreads), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }
 

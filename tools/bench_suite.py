@@ -1,0 +1,125 @@
+"""Device-resident throughput of every BASELINE.json config (not the headline
+line — bench.py is — but the same methodology): HIP events around each
+launch on the launch stream, median of `reps`, algorithmic bytes / time.
+
+    python tools/bench_suite.py [--reps 10] > profiles/<round>_suite.jsonl
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+PEAK = 8000.0
+
+
+def timed(torch, fn, reps):
+    stream = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        fn()
+        b.record(stream)
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    return statistics.median(ts)
+
+
+def row(name, op, ms, alg, payload, extra=None):
+    gbs = alg / ms / 1e6
+    r = {"config": name, "op": op, "ms": round(ms, 4), "alg_GBps": round(gbs, 1),
+         "frac_of_8TBps": round(gbs / PEAK, 4), "payload_GiBps": round(payload / ms * 1e3 / 2**30, 1)}
+    if extra:
+        r.update(extra)
+    print(json.dumps(r), flush=True)
+    return r
+
+
+def stripe_case(torch, le, cls, k, m, w, size, n, reps, erased, repair_ids, name, verify=True):
+    """Objects stored as full stripes [n][(k+m)*bs]: data blocks then coding
+    blocks, so encode / decode / repair all run on one buffer."""
+    bs, _ = le.layout(cls, (k, m, w), size)
+    stride = (k + m) * bs
+    g = torch.Generator(device="cuda").manual_seed(0x1E0E)
+    stripe = torch.zeros((n, stride), dtype=torch.uint8, device="cuda")
+    stripe[:, :size] = torch.randint(0, 256, (n, size), dtype=torch.uint8, device="cuda", generator=g)
+    objs = stripe
+    parity = stripe[:, k * bs:]
+    ref = stripe[:, :size].clone()
+    enc = lambda: le.device.encode(cls, (k, m, w), objs, size, parity)  # noqa: E731
+    t_enc = timed(torch, enc, reps)
+    out = []
+    out.append(row(name, "encode", t_enc, (k + m) * bs * n, size * n))
+    if erased:
+        dec = lambda: le.device.decode(cls, (k, m, w), objs, size, parity, erased)  # noqa: E731
+        t_dec = timed(torch, dec, reps)
+        e = len([x for x in erased if x < k])
+        out.append(row(name, "decode%s" % erased, t_dec, (k + e) * bs * n, size * n))
+        out.append(row(name, "encode+decode", t_enc + t_dec, (2 * k + m + e) * bs * n,
+                       2 * size * n))
+        if verify:
+            stripe[:, :size][:, :e * bs] = 0
+            dec()
+            torch.cuda.synchronize()
+            assert torch.equal(stripe[:, :size], ref), f"{name}: decode mismatch"
+    if repair_ids:
+        blocks = [None if b in repair_ids else stripe[:, b * bs:] for b in range(k + m)]
+        outs = [torch.empty((n, bs), dtype=torch.uint8, device="cuda") for _ in repair_ids]
+        rep = lambda: le.device.repair(cls, (k, m, w), blocks, bs, repair_ids, outs, n)  # noqa
+        t_rep = timed(torch, rep, reps)
+        out.append(row(name, "repair%s" % repair_ids, t_rep, (k + len(repair_ids)) * bs * n,
+                       len(repair_ids) * bs * n))
+        if verify:
+            for i, b in enumerate(repair_ids):
+                assert torch.equal(outs[i], stripe[:, b * bs:(b + 1) * bs]), f"{name}: repair {b}"
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--skip-cpu", action="store_true")
+    args = ap.parse_args()
+    import torch
+
+    import leo_erasure_amd as le
+    torch.cuda.set_device(0)
+    assert le.gf_init() == "ok"
+    MiB = 1 << 20
+    R = args.reps
+    stripe_case(torch, le, "vandrs", 4, 2, 8, MiB, 1024, R, [0, 1], [0, 5],
+                "cfg0: vandrs RS(4,2,8) 1 MiB x1024 (GPU)")
+    stripe_case(torch, le, "vandrs", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], [0, 5, 10, 13],
+                "cfg1/2: vandrs RS(10,4,8) 1 MiB x1024")
+    stripe_case(torch, le, "cauchyrs", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], [0, 5, 10, 13],
+                "cfg3: cauchyrs(10,4,8) bitmatrix 1 MiB x1024")
+    stripe_case(torch, le, "vandrs", 10, 4, 8, 64 * MiB, 16, R, [0, 1, 2, 3], None,
+                "cfg4: vandrs RS(10,4,8) 64 MiB x16 per GPU")
+    stripe_case(torch, le, "isars", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], None,
+                "isars(10,4,8) 1 MiB x1024")
+    stripe_case(torch, le, "liberation", 7, 2, 7, MiB, 1024, R, [0, 1], None,
+                "liberation(7,2,7) 1 MiB x1024")
+    stripe_case(torch, le, "vandrs", 10, 4, 16, MiB, 512, R, [0, 1, 2, 3], None,
+                "vandrs RS(10,4,16) 1 MiB x512")
+    stripe_case(torch, le, "vandrs", 10, 4, 32, MiB, 256, R, [0, 1, 2, 3], None,
+                "vandrs RS(10,4,32) 1 MiB x256")
+    if not args.skip_cpu:
+        import bench
+        threads = min(16, len(os.sched_getaffinity(0)))
+        # config 0 of BASELINE.json: RS(4,2,8) 1 MiB encode+decode on the CPU
+        bench.K, bench.M, bench.ERASED = 4, 2, [0, 1]
+        t0 = time.time()
+        cpu = bench.cpu_baseline(MiB, args.cpu_seconds, threads)
+        print(json.dumps({"config": "cfg0: vandrs RS(4,2,8) 1 MiB encode+decode, CPU port",
+                          "cpu": cpu, "wall_s": round(time.time() - t0, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,82 @@
+"""End-to-end (host memory) encode rates, RS(10,4,8) 1 MiB objects.
+
+The reference path starts and ends in host memory (Erlang binaries), so the
+PCIe-inclusive rate is recorded in DESIGN.md (never as the bench value):
+
+  nif    leoec_encode() per object from pageable memory (the NIF path:
+         H2D object, kernel, D2H parity, synchronous), 1 thread;
+  pinned batched: pinned host objects -> H2D -> leoec_encode_dev -> D2H
+         parity, chunks of `chunk` objects double-buffered on two streams.
+
+    python tools/e2e_bench.py
+"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import numpy as np
+    import torch
+
+    import leo_erasure_amd as le
+    torch.cuda.set_device(0)
+    assert le.gf_init() == "ok"
+    K, M, W, size = 10, 4, 8, 1 << 20
+    bs, filled = le.layout("vandrs", (K, M, W), size)
+
+    # --- NIF path, pageable, one object per call
+    data = np.random.default_rng(1).integers(0, 256, size, dtype=np.uint8).tobytes()
+    for _ in range(3):
+        le.nif_encode("vandrs", (K, M, W), data, size)
+    n = 200
+    t0 = time.perf_counter()
+    for _ in range(n):
+        st, _ = le.nif_encode("vandrs", (K, M, W), data, size)
+        assert st == "ok"
+    t = time.perf_counter() - t0
+    print(json.dumps({"path": "nif leoec_encode, pageable, 1 object/call, 1 thread",
+                      "GiBps": round(n * size / t / 2**30, 2), "us_per_object": round(t / n * 1e6, 1)}))
+
+    # --- pinned, batched, two streams
+    total, chunk = 1024, 64
+    host = torch.randint(0, 256, (total, size), dtype=torch.uint8).pin_memory()
+    hpar = torch.empty((total, M * bs), dtype=torch.uint8).pin_memory()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    dobj = [torch.empty((chunk, size), dtype=torch.uint8, device="cuda") for _ in streams]
+    dpar = [torch.empty((chunk, M * bs), dtype=torch.uint8, device="cuda") for _ in streams]
+
+    def run():
+        for i, c0 in enumerate(range(0, total, chunk)):
+            s = streams[i % 2]
+            with torch.cuda.stream(s):
+                dobj[i % 2].copy_(host[c0:c0 + chunk], non_blocking=True)
+                le.device.encode("vandrs", (K, M, W), dobj[i % 2], size, dpar[i % 2],
+                                 stream=s.cuda_stream)
+                hpar[c0:c0 + chunk].copy_(dpar[i % 2], non_blocking=True)
+        torch.cuda.synchronize()
+
+    run()
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        run()
+    t = (time.perf_counter() - t0) / reps
+    h2d = total * size
+    d2h = total * M * bs
+    print(json.dumps({"path": "pinned batched H2D+encode+D2H (2 streams, 64-object chunks)",
+                      "GiBps_payload": round(total * size / t / 2**30, 2),
+                      "pcie_GBps": round((h2d + d2h) / t / 1e9, 2), "ms": round(t * 1e3, 2)}))
+    # spot-check one object's parity against a fresh device encode
+    dev = host[:1].cuda()
+    p = torch.empty((1, M * bs), dtype=torch.uint8, device="cuda")
+    le.device.encode("vandrs", (K, M, W), dev, size, p)
+    torch.cuda.synchronize()
+    assert torch.equal(p.cpu(), hpar[:1])
+
+
+if __name__ == "__main__":
+    main()

@@ -11,6 +11,14 @@ for p in "${PARTS[@]}"; do
     variants) step variants 600 python tools/kvariants.py ${KV_ARGS:-} ;;
     pytest) step pytest 1200 python -m pytest tests -x -q -m gpu ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    suite) step suite 900 python tools/bench_suite.py ${SUITE_ARGS:-} ;;
+    e2e) step e2e 600 python tools/e2e_bench.py ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    counters)
+      cd /tmp && export TMPDIR=/tmp
+      step counters_list 300 rocprofv3 -L
+      step pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_sq" -o run -- python "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu
+      cd "$ROOT" ;;
     pmc)
       cd /tmp && export TMPDIR=/tmp
       step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu

@@ -11,8 +11,9 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-NAMES = {1: "shipped (cpt1 nt)", 11: "nt+branchfree", 12: "no-nt", 2: "cpt2", 3: "nt", 4: "cpt2+nt", 5: "branchfree", 6: "copy-xor",
-         7: "copy-xor+nt", 8: "cpt2+branchfree", 9: "cpt4", 10: "copy-xor cpt2"}
+NAMES = {1: "shipped (auto branchy/paired)", 2: "cpt2", 3: "always-branchy", 5: "always-paired",
+         7: "copy-xor", 12: "no-nt", 13: "persistent-prefetch", 14: "copy-xor persistent"}
+DEFAULT = [1, 3, 5, 7, 12, 13, 14]
 
 
 def main():
