@@ -36,8 +36,8 @@ def shard_range(rank, world, total):
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=30)
     p.add_argument("--objects", type=int, default=1024, help="1 MiB objects per GPU")
     p.add_argument("--size", type=int, default=1048576)
     p.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -77,8 +77,8 @@ def cpu_baseline(size, target_s, threads, sample_objs=2048):
     return {
         "value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
         "simd": {0: "scalar", 2: "avx2-pshufb"}.get(O.simd_level(), "scalar"),
-        "sample": f"{passes} passes over {n} x {size} B objects: vandrs RS(10,4,8) encode "
-                  f"{te:.2f} s + in-place-equivalent decode of {{0,1,2,3}} {td:.2f} s, "
+        "sample": f"{passes} passes over {n} x {size} B objects: vandrs RS({K},{M},8) encode "
+                  f"{te:.2f} s + in-place decode of data blocks {ERASED} {td:.2f} s, "
                   f"{threads} threads",
     }
 
@@ -138,8 +138,10 @@ def main(argv=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
-    dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+    enc_t = [e[0].elapsed_time(e[1]) for e in events]
+    dec_t = [e[1].elapsed_time(e[2]) for e in events]
+    enc_ms = sum(enc_t) / args.steps
+    dec_ms = sum(dec_t) / args.steps
     # decode rebuilt blocks 0..3 in place every step: the batch must be intact
     intact = bool(torch.equal(objs, ref))
     if world > 1:
@@ -190,6 +192,8 @@ def main(argv=None):
                 "decode": {"achieved": round(dec_gbs, 1), "frac": round(dec_gbs / HBM_PEAK_GBS, 4),
                            "alg_bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_ms, 4)},
             },
+            "kernel_ms": {"encode_min_med_max": [round(x, 4) for x in (min(enc_t), sorted(enc_t)[len(enc_t) // 2], max(enc_t))],
+                          "decode_min_med_max": [round(x, 4) for x in (min(dec_t), sorted(dec_t)[len(dec_t) // 2], max(dec_t))]},
             "verified": intact,
         }
         if world == 1 and not args.no_cpu:

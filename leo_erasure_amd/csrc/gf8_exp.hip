@@ -7,16 +7,18 @@ namespace leoec {
 namespace detail {
 
 ChunkFn gf8_variant(int v) {
-  //                            K   R  ACC    CPT  NT     BRANCHY COPY   PIPE
+  //                             K   R  ACC    CPT NT    BR  COPY   PIPE   LDS
   switch (v) {
-    case 1: return &launch_gf8_t<10, 4, false, 1, true, -1, false, false>;  // shipped
-    case 2: return &launch_gf8_t<10, 4, false, 2, true, -1, false, false>;
-    case 3: return &launch_gf8_t<10, 4, false, 1, true, 1, false, false>;   // always branchy
-    case 5: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false>;   // always paired
-    case 7: return &launch_gf8_t<10, 4, false, 1, true, 1, true, false>;    // copy-xor
-    case 12: return &launch_gf8_t<10, 4, false, 1, false, -1, false, false>;  // no nt
-    case 13: return &launch_gf8_t<10, 4, false, 1, true, -1, false, true>;  // persistent prefetch
-    case 14: return &launch_gf8_t<10, 4, false, 1, true, 1, true, true>;    // copy-xor persistent
+    case 1: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true>;   // shipped
+    case 2: return &launch_gf8_t<10, 4, false, 2, true, 0, false, false, true>;   // cpt2
+    case 3: return &launch_gf8_t<10, 4, false, 1, true, 1, false, false, false>;  // branchy sgpr
+    case 4: return &launch_gf8_t<10, 4, false, 1, true, 1, false, false, true>;   // branchy lds
+    case 5: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, false>;  // paired sgpr
+    case 7: return &launch_gf8_t<10, 4, false, 1, true, 1, true, false, false>;   // copy-xor
+    case 12: return &launch_gf8_t<10, 4, false, 1, false, 0, false, false, true>; // no nt
+    case 15: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5>;  // >=5 waves
+    case 16: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 6>;  // >=6 waves
+    case 17: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 8>;  // 8 waves
     default: return nullptr;
   }
 }

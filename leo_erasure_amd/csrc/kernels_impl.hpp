@@ -129,12 +129,15 @@ struct Gf8Args {
 // Kernel shape / policy knobs (the engine ships kGf8Default; the others exist
 // for A/B measurement through LEOEC_GF8_VARIANT, see tools/kvariants.py).
 struct Gf8Opt {
-  int cpt;       // 16-byte columns per lane (tile = 4 KiB * cpt per block)
-  bool nt;       // non-temporal loads / stores (streamed once, never re-read)
-  bool branchy;  // scalar branch on coefficients 0 / 1 instead of table lookups
-  bool copy;     // measurement only: same traffic, XOR instead of GF multiply
+  int cpt;      // 16-byte columns per lane (tile = 4 KiB * cpt per block)
+  bool nt;      // non-temporal loads / stores (streamed once, never re-read)
+  int branchy;  // 1: scalar branch on coefficients 0 / 1; 0: all tables, xor3-paired;
+                // -1: pick per launch from the coefficients
+  bool copy;    // measurement only: same traffic, XOR instead of GF multiply
+  bool lds;     // perm tables staged in LDS (VGPR operands) instead of SGPRs
+  int waves;    // minimum waves per SIMD requested from the register allocator
 };
-constexpr Gf8Opt kGf8Default{1, true, true, false};
+constexpr Gf8Opt kGf8Default{1, true, 0, false, true, 5};
 
 
 // One tile of the GF(2^8) map for columns already loaded in d.
@@ -142,9 +145,16 @@ constexpr Gf8Opt kGf8Default{1, true, true, false};
 //           3 perm + xor3 + xor;
 //  !BRANCHY: every coefficient through its tables, with the 3K perm outputs
 //           of a row folded pairwise by xor3 (1.5 ops per coefficient).
-template <int K, int R, int CPT, bool BRANCHY, bool COPY>
-__device__ __forceinline__ void gf8_tile(const Gf8Args<K, R>& a, const u32x4 (&d)[CPT][K],
-                                         u32x4 (&acc)[CPT][R]) {
+// Per-coefficient v_perm tables staged in LDS: [t0 lo, t0 hi, t1 lo, t1 hi]
+// and [t2, -, -, -] (32 bytes per coefficient, 16-byte aligned).
+template <int K, int R>
+struct Gf8Lds {
+  u32x4 t[R * K][2];
+};
+
+template <int K, int R, int CPT, bool BRANCHY, bool COPY, bool LDS>
+__device__ __forceinline__ void gf8_tile(const Gf8Args<K, R>& a, const Gf8Lds<K, R>& lds,
+                                         const u32x4 (&d)[CPT][K], u32x4 (&acc)[CPT][R]) {
   u32x4 pend[CPT][R];
 #pragma unroll
   for (int j = 0; j < K; ++j) {
@@ -172,9 +182,16 @@ __device__ __forceinline__ void gf8_tile(const Gf8Args<K, R>& a, const u32x4 (&d
 #pragma unroll
         for (int c = 0; c < CPT; ++c) acc[c][r] ^= d[c][j];
       } else if (!BRANCHY || !((a.zero >> bit) & 1)) {
-        const uint32_t t0l = a.tab[r][j][0], t0h = a.tab[r][j][1];
-        const uint32_t t1l = a.tab[r][j][2], t1h = a.tab[r][j][3];
-        const uint32_t t2 = a.tab[r][j][4];
+        uint32_t t0l, t0h, t1l, t1h, t2;
+        if (LDS) {  // VGPR operands: no SGPR pressure, no constant-bus moves
+          const u32x4 t = lds.t[r * K + j][0];
+          t0l = t[0]; t0h = t[1]; t1l = t[2]; t1h = t[3];
+          t2 = lds.t[r * K + j][1][0];
+        } else {
+          t0l = a.tab[r][j][0]; t0h = a.tab[r][j][1];
+          t1l = a.tab[r][j][2]; t1h = a.tab[r][j][3];
+          t2 = a.tab[r][j][4];
+        }
 #pragma unroll
         for (int c = 0; c < CPT; ++c)
 #pragma unroll
@@ -259,9 +276,20 @@ __device__ __forceinline__ void gf8_store(const Gf8Args<K, R>& a, uint64_t o, ui
 // One workgroup per tile (PIPE = false), or a persistent grid that walks the
 // tiles and issues the loads of its next tile before computing the current
 // one (PIPE = true).
-template <int K, int R, bool ACC, int CPT, bool NT, bool BRANCHY, bool COPY, bool PIPE>
-__global__ void __launch_bounds__(kThreads) gf8_apply(const Gf8Args<K, R> a) {
+template <int K, int R, bool ACC, int CPT, bool NT, bool BRANCHY, bool COPY, bool PIPE, bool LDS,
+          int WAVES>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
+gf8_apply(const Gf8Args<K, R> a) {
   constexpr uint32_t TB = kTileBytes * CPT;
+  __shared__ Gf8Lds<K, R> lds;
+  if (LDS) {
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(R * K); i += kThreads) {
+      const uint32_t* t = a.tab[i / K][i % K];
+      lds.t[i][0] = u32x4{t[0], t[1], t[2], t[3]};
+      lds.t[i][1] = u32x4{t[4], 0u, 0u, 0u};
+    }
+    __syncthreads();
+  }
   if (!PIPE) {
     const uint32_t obj = blockIdx.x / a.tiles;
     const uint32_t tile = blockIdx.x - obj * a.tiles;
@@ -272,7 +300,7 @@ __global__ void __launch_bounds__(kThreads) gf8_apply(const Gf8Args<K, R> a) {
     gf8_load<K, R, CPT, NT>(a, obj, off, full, d);
     u32x4 acc[CPT][R];
     gf8_init_store<K, R, ACC, CPT, NT>(a, obj, off, acc);
-    gf8_tile<K, R, CPT, BRANCHY, COPY>(a, d, acc);
+    gf8_tile<K, R, CPT, BRANCHY, COPY, LDS>(a, lds, d, acc);
     gf8_store<K, R, CPT, NT>(a, obj, off, full, acc);
     return;
   }
@@ -302,7 +330,7 @@ __global__ void __launch_bounds__(kThreads) gf8_apply(const Gf8Args<K, R> a) {
     }
     u32x4 acc[CPT][R];
     gf8_init_store<K, R, ACC, CPT, NT>(a, cobj, coff, acc);
-    gf8_tile<K, R, CPT, BRANCHY, COPY>(a, d, acc);
+    gf8_tile<K, R, CPT, BRANCHY, COPY, LDS>(a, lds, d, acc);
     gf8_store<K, R, CPT, NT>(a, cobj, coff, cfull, acc);
     if (!more) break;
   }
@@ -469,7 +497,8 @@ int device_cus();  // compute units of the current device (kernels.hip)
 // BRANCHY = -1: pick per launch from the coefficients (scalar-branch form
 // when enough coefficients are 0/1, the paired all-table form otherwise).
 template <int K, int R, bool ACC, int CPT = kGf8Default.cpt, bool NT = kGf8Default.nt,
-          int BRANCHY = -1, bool COPY = kGf8Default.copy, bool PIPE = false>
+          int BRANCHY = kGf8Default.branchy, bool COPY = kGf8Default.copy, bool PIPE = false,
+          bool LDS = kGf8Default.lds, int WAVES = kGf8Default.waves>
 int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   Gf8Args<K, R> a;
   a.one = a.zero = 0;
@@ -504,10 +533,10 @@ int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
     grid = grid < cap ? grid : cap;
   }
   if (branchy)
-    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, true, COPY, PIPE>), dim3(grid),
+    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, true, COPY, PIPE, LDS, WAVES>), dim3(grid),
                        dim3(kThreads), 0, s, a);
   else
-    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, false, COPY, PIPE>), dim3(grid),
+    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, false, COPY, PIPE, LDS, WAVES>), dim3(grid),
                        dim3(kThreads), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }

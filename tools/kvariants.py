@@ -11,9 +11,10 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-NAMES = {1: "shipped (auto branchy/paired)", 2: "cpt2", 3: "always-branchy", 5: "always-paired",
-         7: "copy-xor", 12: "no-nt", 13: "persistent-prefetch", 14: "copy-xor persistent"}
-DEFAULT = [1, 3, 5, 7, 12, 13, 14]
+NAMES = {1: "shipped (lds+paired)", 2: "cpt2", 3: "branchy sgpr", 4: "branchy lds",
+         5: "paired sgpr", 7: "copy-xor", 12: "no-nt", 15: "waves>=5", 16: "waves>=6 (spills)",
+         17: "waves 8 (spills)"}
+DEFAULT = [1, 5, 7, 15, 16]
 
 
 def main():
@@ -22,6 +23,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default=",".join(str(v) for v in DEFAULT))
     ap.add_argument("--objects", type=int, default=1024)
+    ap.add_argument("--burst", action="store_true",
+                    help="launch the reps back to back, synchronise once (bench-like)")
     args = ap.parse_args()
     import torch
     import leo_erasure_amd as le
@@ -44,6 +47,7 @@ def main():
     for rnd in range(args.rounds):
         for v in variants:
             os.environ["LEOEC_GF8_VARIANT"] = str(v)
+            evs = []
             for _ in range(args.reps):
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
                 e[0].record(stream)
@@ -51,7 +55,11 @@ def main():
                 e[1].record(stream)
                 le.device.decode("vandrs", (K, M, W), objs, size, parity, [0, 1, 2, 3])
                 e[2].record(stream)
-                torch.cuda.synchronize()
+                if not args.burst:
+                    torch.cuda.synchronize()
+                evs.append(e)
+            torch.cuda.synchronize()
+            for e in evs:
                 res[v]["enc"].append(e[0].elapsed_time(e[1]))
                 res[v]["dec"].append(e[1].elapsed_time(e[2]))
             if NAMES.get(v, "").startswith("copy"):
