@@ -7,6 +7,7 @@
 #include "engine.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -192,12 +193,36 @@ int bit_rows(const Code& c, const int* surv, const int* want, int nwant,
   return LEOEC_OK;
 }
 
+namespace {
+// LEOEC_BITMATRIX=1 forces the generic masked-bitmatrix kernel for cauchyrs
+// (measurement / cross-check of the bitsliced GF path).
+int bitmatrix_env() {
+  const char* e = std::getenv("LEOEC_BITMATRIX");
+  return e ? std::atoi(e) : 0;
+}
+}  // namespace
+
 int apply(const Code& c, const int* surv, const std::vector<Shard>& in, const int* want,
           const std::vector<Shard>& out, uint64_t bs, uint64_t nobj, hipStream_t s) {
   const int nwant = (int)out.size();
   if (nwant == 0 || nobj == 0 || bs == 0) return LEOEC_OK;
   if (!c.bitmatrix) {
     GfApply p;
+    p.w = c.w;
+    p.K = c.k;
+    p.R = nwant;
+    int rc = gf_rows(c, surv, want, nwant, &p.coef);
+    if (rc) return rc;
+    p.in = in;
+    p.out = out;
+    p.block_size = bs;
+    p.nobj = nobj;
+    return launch(p, s);
+  }
+  if (c.coding == LEOEC_CAUCHYRS && gfbit_supported(c.w) && bitmatrix_env() == 0) {
+    // cauchyrs bitmatrices (coding and decoding) are bit expansions of GF(2^w)
+    // matrices: apply the GF map on the packet-bitsliced blocks directly
+    GfBitApply p;
     p.w = c.w;
     p.K = c.k;
     p.R = nwant;

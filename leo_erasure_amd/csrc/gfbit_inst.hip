@@ -1,0 +1,113 @@
+// gfbit_inst.hip — launches of the packet-bitsliced GF(2^w) kernel
+// (kernels_impl.hpp gfbit_apply) for w = 2..16, R <= 4 outputs per launch,
+// inputs beyond 16 folded in by accumulating launches.
+#include <cstdlib>
+#include <utility>
+
+#include "kernels_impl.hpp"
+
+namespace leoec {
+
+using namespace detail;
+
+namespace {
+
+using GfbFn = int (*)(const GfBitApply&, int r0, int j0, int nk, uint64_t o0, uint64_t no,
+                      hipStream_t);
+
+template <int W, int R, int LW, bool ACC>
+int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
+                 hipStream_t s) {
+  GfbArgs<R> a;
+  a.K = nk;
+  a.ps = (uint32_t)(p.block_size / (uint64_t)W);
+  constexpr uint32_t tb = kThreads * 4u * LW;
+  a.tiles = (a.ps + tb - 1) / tb;
+  for (int j = 0; j < kMaxK; ++j)
+    a.in[j] = j < nk ? dev_shard(p.in[j0 + j], o0) : DevShard{nullptr, 0, 0, 0};
+  for (int i = 0; i < R; ++i) {
+    a.out[i] = dev_shard(p.out[r0 + i], o0);
+    for (int j = 0; j < kMaxK; ++j)
+      a.coef[i][j] = j < nk ? p.coef[(size_t)(r0 + i) * p.K + j0 + j] : 0u;
+  }
+  hipLaunchKernelGGL((gfbit_apply<W, R, LW, ACC>), dim3((uint32_t)(no * a.tiles)),
+                     dim3(kThreads), 0, s, a);
+  return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
+}
+
+template <int W, int LW>
+GfbFn pick_r(int r, bool acc) {
+  static const GfbFn tbl[2][kMaxR] = {
+      {&launch_gfb_t<W, 1, LW, false>, &launch_gfb_t<W, 2, LW, false>,
+       &launch_gfb_t<W, 3, LW, false>, &launch_gfb_t<W, 4, LW, false>},
+      {&launch_gfb_t<W, 1, LW, true>, &launch_gfb_t<W, 2, LW, true>,
+       &launch_gfb_t<W, 3, LW, true>, &launch_gfb_t<W, 4, LW, true>}};
+  return tbl[acc ? 1 : 0][r - 1];
+}
+
+// LEOEC_GFBIT_LW=1|2|4 selects the lane width (dwords per packet per lane)
+// for w = 8 measurements; the shipped width is 2.
+int lane_width_env() {
+  const char* e = std::getenv("LEOEC_GFBIT_LW");
+  return e ? std::atoi(e) : 2;
+}
+
+GfbFn pick(int w, int r, bool acc) {
+  if (w == 8) {
+    const int lw = lane_width_env();
+    if (lw == 1) return pick_r<8, 1>(r, acc);
+    if (lw == 4) return pick_r<8, 4>(r, acc);
+    return pick_r<8, 2>(r, acc);
+  }
+  switch (w) {
+    case 2: return pick_r<2, 2>(r, acc);
+    case 3: return pick_r<3, 2>(r, acc);
+    case 4: return pick_r<4, 2>(r, acc);
+    case 5: return pick_r<5, 2>(r, acc);
+    case 6: return pick_r<6, 2>(r, acc);
+    case 7: return pick_r<7, 2>(r, acc);
+    case 9: return pick_r<9, 2>(r, acc);
+    case 10: return pick_r<10, 2>(r, acc);
+    case 11: return pick_r<11, 2>(r, acc);
+    case 12: return pick_r<12, 1>(r, acc);
+    case 13: return pick_r<13, 1>(r, acc);
+    case 14: return pick_r<14, 1>(r, acc);
+    case 15: return pick_r<15, 1>(r, acc);
+    case 16: return pick_r<16, 1>(r, acc);
+    default: return nullptr;
+  }
+}
+
+}  // namespace
+
+bool gfbit_supported(int w) { return w >= 2 && w <= 16; }
+
+int launch(const GfBitApply& p, hipStream_t s) {
+  const int w = p.w;
+  if (!gfbit_supported(w) || p.K <= 0 || p.R <= 0 || (int)p.in.size() != p.K ||
+      (int)p.out.size() != p.R || p.coef.size() != (size_t)p.K * p.R)
+    return LEOEC_E_ARG;
+  if (p.block_size == 0 || p.nobj == 0) return LEOEC_OK;
+  if (p.block_size % ((uint64_t)16 * w) || p.block_size >= (1ull << 32)) return LEOEC_E_BAD_SIZE;
+  for (const Shard& sh : p.in)
+    if (((uintptr_t)sh.base & 15u) || (sh.stride & 15u)) return LEOEC_E_ARG;
+  for (const Shard& sh : p.out)
+    if (((uintptr_t)sh.base & 15u) || (sh.stride & 15u)) return LEOEC_E_ARG;
+  const uint64_t ps = p.block_size / (uint64_t)w;
+  const uint64_t tiles = (ps + 1023) / 1024;  // smallest lane width -> most tiles
+  const uint64_t max_obj = (uint64_t)0x7FFFFFFF / tiles;
+  for (uint64_t o0 = 0; o0 < p.nobj; o0 += max_obj) {
+    const uint64_t no = (p.nobj - o0 < max_obj) ? p.nobj - o0 : max_obj;
+    for (int r0 = 0; r0 < p.R; r0 += kMaxR) {
+      const int nr = (p.R - r0 < kMaxR) ? p.R - r0 : kMaxR;
+      for (int j0 = 0; j0 < p.K; j0 += kMaxK) {
+        const int nk = (p.K - j0 < kMaxK) ? p.K - j0 : kMaxK;
+        const int rc = pick(w, nr, j0 > 0)(p, r0, j0, nk, o0, no, s);
+        if (rc) return rc;
+      }
+    }
+  }
+  return LEOEC_OK;
+}
+
+}  // namespace leoec

@@ -46,8 +46,24 @@ struct BitApply {
   uint64_t nobj = 0;
 };
 
+// A GF(2^w) matrix applied to packet-bitsliced blocks: block = w packets of
+// block_size / w bytes, packet x holding bit x of every symbol.  This is the
+// bitmatrix product of the matrix's bit expansion (cauchyrs, whose coding
+// and decoding bitmatrices are expansions of GF(2^w) matrices), computed as
+// sum over set coefficient bits t of (block * 2^t), with *2 done on packets.
+struct GfBitApply {
+  int w = 0;
+  int K = 0, R = 0;
+  std::vector<uint32_t> coef;  // R x K
+  std::vector<Shard> in, out;
+  uint64_t block_size = 0;     // multiple of 16*w
+  uint64_t nobj = 0;
+};
+
 // Enqueue on `stream`; returns a leoec_status.
 int launch(const GfApply& plan, hipStream_t stream);
 int launch(const BitApply& plan, hipStream_t stream);
+int launch(const GfBitApply& plan, hipStream_t stream);
+bool gfbit_supported(int w);
 
 }  // namespace leoec

@@ -454,6 +454,172 @@ __global__ void __launch_bounds__(kThreads) bit_apply(const BitArgs a) {
 }
 
 // ===========================================================================
+// GF(2^w) on packet-bitsliced blocks (cauchyrs).  Each lane owns LW dwords of
+// every packet.  Per input block: y = its w packets; for t = 0..w-1, every
+// output block whose coefficient has bit t set gets y xor-ed in, then
+// y <- y * 2 in bitsliced form (a rename plus one xor per set low bit of the
+// primitive polynomial).  Cost per packet dword ~ popcount(coef) + 3, against
+// m*w masked xors for a generic bitmatrix.
+template <int R>
+struct GfbArgs {
+  DevShard in[kMaxK];
+  DevShard out[R];
+  uint32_t coef[R][kMaxK];
+  int K;
+  uint32_t ps;     // packet bytes
+  uint32_t tiles;  // tiles per object (over one packet)
+};
+
+template <int W>
+struct DefaultPoly;  // low bits of the gf-complete default polynomial
+template <> struct DefaultPoly<2> { static constexpr uint32_t v = 03; };
+template <> struct DefaultPoly<3> { static constexpr uint32_t v = 03; };
+template <> struct DefaultPoly<4> { static constexpr uint32_t v = 03; };
+template <> struct DefaultPoly<5> { static constexpr uint32_t v = 05; };
+template <> struct DefaultPoly<6> { static constexpr uint32_t v = 03; };
+template <> struct DefaultPoly<7> { static constexpr uint32_t v = 011; };
+template <> struct DefaultPoly<8> { static constexpr uint32_t v = 035; };
+template <> struct DefaultPoly<9> { static constexpr uint32_t v = 021; };
+template <> struct DefaultPoly<10> { static constexpr uint32_t v = 011; };
+template <> struct DefaultPoly<11> { static constexpr uint32_t v = 05; };
+template <> struct DefaultPoly<12> { static constexpr uint32_t v = 0123; };
+template <> struct DefaultPoly<13> { static constexpr uint32_t v = 033; };
+template <> struct DefaultPoly<14> { static constexpr uint32_t v = 02103; };
+template <> struct DefaultPoly<15> { static constexpr uint32_t v = 03; };
+template <> struct DefaultPoly<16> { static constexpr uint32_t v = 010013; };
+
+template <int LW>
+struct LaneVec {
+  uint32_t v[LW];
+};
+
+template <int LW>
+__device__ __forceinline__ LaneVec<LW> lv_load(const uint8_t* p, uint32_t off, uint32_t valid) {
+  LaneVec<LW> r;
+  if (LW == 4) {
+    const u32x4 x = load_guarded(p, off, valid);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r.v[e] = x[e];
+  } else {
+    typedef uint32_t vt __attribute__((ext_vector_type(LW == 1 ? 1 : 2)));
+    const uint32_t bytes = 4u * LW;
+    if (off + bytes <= valid) {
+      if (LW == 2) {
+        const vt x = __builtin_nontemporal_load(reinterpret_cast<const vt*>(p + off));
+        r.v[0] = x[0];
+        r.v[LW - 1] = x[LW == 2 ? 1 : 0];
+      } else {
+        r.v[0] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p + off));
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < LW; ++e) {
+        const uint32_t o = off + 4u * e;
+        uint32_t w = 0;
+        if (o < valid) {
+          w = *reinterpret_cast<const uint32_t*>(p + o);
+          const uint32_t n = valid - o;
+          if (n < 4) w &= (1u << (8u * n)) - 1u;
+        }
+        r.v[e] = w;
+      }
+    }
+  }
+  return r;
+}
+
+template <int LW>
+__device__ __forceinline__ void lv_store(uint8_t* p, uint32_t off, uint32_t valid,
+                                         const LaneVec<LW>& x) {
+  const uint32_t bytes = 4u * LW;
+  if (off + bytes <= valid) {
+    if (LW == 4) {
+      st16<true>(p + off, u32x4{x.v[0], x.v[1 % LW], x.v[2 % LW], x.v[3 % LW]});
+    } else if (LW == 2) {
+      typedef uint32_t v2 __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store(v2{x.v[0], x.v[LW - 1]}, reinterpret_cast<v2*>(p + off));
+    } else {
+      __builtin_nontemporal_store(x.v[0], reinterpret_cast<uint32_t*>(p + off));
+    }
+  } else if (off < valid) {
+    const uint32_t n = valid - off;
+#pragma unroll
+    for (int i = 0; i < 4 * LW; ++i)
+      if ((uint32_t)i < n) p[off + i] = (uint8_t)(x.v[i >> 2] >> (8 * (i & 3)));
+  }
+}
+
+template <int W, int R, int LW, bool ACC>
+__global__ void __launch_bounds__(kThreads) gfbit_apply(const GfbArgs<R> a) {
+  constexpr uint32_t LB = 4u * LW;
+  const uint32_t obj = blockIdx.x / a.tiles;
+  const uint32_t tile = blockIdx.x - obj * a.tiles;
+  const uint32_t off = tile * (kThreads * LB) + threadIdx.x * LB;
+  if (off >= a.ps) return;
+  const uint64_t o64 = obj;
+  LaneVec<LW> acc[R][W];
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      if (ACC) {
+        const uint32_t pk = (uint32_t)x * a.ps;
+        const uint32_t bv = a.out[i].valid;
+        acc[i][x] = lv_load<LW>(a.out[i].base + o64 * a.out[i].stride + pk, off,
+                                bv > pk ? bv - pk : 0u);
+      } else {
+#pragma unroll
+        for (int e = 0; e < LW; ++e) acc[i][x].v[e] = 0u;
+      }
+    }
+  for (int j = 0; j < a.K; ++j) {
+    const uint8_t* base = a.in[j].base + o64 * a.in[j].stride;
+    const uint32_t bv = a.in[j].valid;
+    LaneVec<LW> y[W];
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const uint32_t pk = (uint32_t)x * a.ps;
+      y[x] = lv_load<LW>(base + pk, off, bv > pk ? bv - pk : 0u);
+    }
+    uint32_t c[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) c[i] = a.coef[i][j];
+#pragma unroll
+    for (int t = 0; t < W; ++t) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        if ((c[i] >> t) & 1u) {
+#pragma unroll
+          for (int x = 0; x < W; ++x)
+#pragma unroll
+            for (int e = 0; e < LW; ++e) acc[i][x].v[e] ^= y[x].v[e];
+        }
+      }
+      if (t + 1 < W) {  // y <- y * 2
+        const LaneVec<LW> top = y[W - 1];
+#pragma unroll
+        for (int r = W - 1; r >= 1; --r) {
+#pragma unroll
+          for (int e = 0; e < LW; ++e)
+            y[r].v[e] = ((DefaultPoly<W>::v >> r) & 1u) ? (y[r - 1].v[e] ^ top.v[e]) : y[r - 1].v[e];
+        }
+        y[0] = top;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    uint8_t* p = const_cast<uint8_t*>(a.out[i].base) + o64 * a.out[i].stride;
+    const uint32_t bv = a.out[i].valid;
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const uint32_t pk = (uint32_t)x * a.ps;
+      lv_store<LW>(p + pk, off, bv > pk ? bv - pk : 0u, acc[i][x]);
+    }
+  }
+}
+
+// ===========================================================================
 // Host-side launch templates.
 inline DevShard dev_shard(const Shard& s, uint64_t o0) {
   DevShard d;

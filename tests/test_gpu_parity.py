@@ -251,3 +251,33 @@ def test_device_roundtrip_bench_shape(gpu, le):
     objs[:, : 4 * bs] = 0
     le.device.decode("vandrs", (k, m, w), objs, size, parity, [0, 1, 2, 3])
     assert gpu.equal(objs, ref)
+
+
+@pytest.mark.parametrize("env", [{"LEOEC_BITMATRIX": "1"}, {"LEOEC_GFBIT_LW": "1"},
+                                 {"LEOEC_GFBIT_LW": "4"}], ids=lambda e: ",".join(e))
+def test_cauchy_kernel_forms_agree(gpu, le, oracle, env, monkeypatch):
+    """cauchyrs through the generic masked-bitmatrix kernel and through every
+    lane width of the bitsliced GF kernel gives the oracle's bytes."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for cls, k, m, w in [("cauchyrs", 10, 4, 8), ("cauchyrs", 6, 3, 4), ("cauchyrs", 4, 2, 3)]:
+        data = rand_bytes(100003, k + m + w)
+        st, blocks = le.nif_encode(cls, (k, m, w), data, len(data))
+        assert st == "ok" and blocks == oracle.encode(cls, k, m, w, data)
+        ids = list(range(m, k + m))
+        st, out = le.nif_decode(cls, (k, m, w), [blocks[i] for i in ids], ids, len(data))
+        assert st == "ok" and out == data
+
+
+def test_golden_fixtures_gpu(gpu, le):
+    """The committed restatement-derived fixtures, through the GPU engine."""
+    import json
+    import os
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with open(os.path.join(here, "index.json")) as fh:
+        index = json.load(fh)
+    for ent in index:
+        z = np.load(os.path.join(here, ent["file"]), allow_pickle=False)
+        st, blocks = le.nif_encode(ent["class"], (ent["k"], ent["m"], ent["w"]),
+                                   z["data"].tobytes(), ent["size"])
+        assert st == "ok" and b"".join(blocks) == z["blocks"].tobytes(), ent["file"]

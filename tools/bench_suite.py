@@ -100,6 +100,13 @@ def main():
                 "cfg1/2: vandrs RS(10,4,8) 1 MiB x1024")
     stripe_case(torch, le, "cauchyrs", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], [0, 5, 10, 13],
                 "cfg3: cauchyrs(10,4,8) bitmatrix 1 MiB x1024")
+    for env, label in [({"LEOEC_GFBIT_LW": "1"}, "lane 4 B"), ({"LEOEC_GFBIT_LW": "4"}, "lane 16 B"),
+                       ({"LEOEC_BITMATRIX": "1"}, "masked bitmatrix kernel")]:
+        os.environ.update(env)
+        stripe_case(torch, le, "cauchyrs", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], None,
+                    "cfg3 variant (%s): cauchyrs(10,4,8) 1 MiB x1024" % label)
+        for k in env:
+            os.environ.pop(k)
     stripe_case(torch, le, "vandrs", 10, 4, 8, 64 * MiB, 16, R, [0, 1, 2, 3], None,
                 "cfg4: vandrs RS(10,4,8) 64 MiB x16 per GPU")
     stripe_case(torch, le, "isars", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], None,
