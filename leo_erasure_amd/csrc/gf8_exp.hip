@@ -19,6 +19,11 @@ ChunkFn gf8_variant(int v) {
     case 15: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5>;  // >=5 waves
     case 16: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 6>;  // >=6 waves
     case 17: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 8>;  // 8 waves
+    case 20: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 512>;
+    case 21: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 256, true>;
+    case 22: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 512, true>;
+    case 23: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 1024>;
+    case 24: return &launch_gf8_t<10, 4, false, 1, true, 1, true, false, false, 5, 256, true>;  // copy xmap
     default: return nullptr;
   }
 }

@@ -220,9 +220,10 @@ __device__ __forceinline__ void gf8_tile(const Gf8Args<K, R>& a, const Gf8Lds<K,
   }
 }
 
-template <int K, int R, int CPT, bool NT>
+template <int K, int R, int CPT, bool NT, uint32_t CS = kTileBytes>
 __device__ __forceinline__ void gf8_load(const Gf8Args<K, R>& a, uint64_t o, uint32_t off,
                                          bool full, u32x4 (&d)[CPT][K]) {
+  constexpr uint32_t kTileBytes = CS;
   if (full) {
 #pragma unroll
     for (int j = 0; j < K; ++j)
@@ -239,9 +240,10 @@ __device__ __forceinline__ void gf8_load(const Gf8Args<K, R>& a, uint64_t o, uin
   }
 }
 
-template <int K, int R, bool ACC, int CPT, bool NT>
+template <int K, int R, bool ACC, int CPT, bool NT, uint32_t CS = kTileBytes>
 __device__ __forceinline__ void gf8_init_store(const Gf8Args<K, R>& a, uint64_t o, uint32_t off,
                                                u32x4 (&acc)[CPT][R]) {
+  constexpr uint32_t kTileBytes = CS;
 #pragma unroll
   for (int c = 0; c < CPT; ++c)
 #pragma unroll
@@ -253,9 +255,10 @@ __device__ __forceinline__ void gf8_init_store(const Gf8Args<K, R>& a, uint64_t 
     }
 }
 
-template <int K, int R, int CPT, bool NT>
+template <int K, int R, int CPT, bool NT, uint32_t CS = kTileBytes>
 __device__ __forceinline__ void gf8_store(const Gf8Args<K, R>& a, uint64_t o, uint32_t off,
                                           bool full, const u32x4 (&acc)[CPT][R]) {
+  constexpr uint32_t kTileBytes = CS;
   if (full) {
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -276,14 +279,26 @@ __device__ __forceinline__ void gf8_store(const Gf8Args<K, R>& a, uint64_t o, ui
 // One workgroup per tile (PIPE = false), or a persistent grid that walks the
 // tiles and issues the loads of its next tile before computing the current
 // one (PIPE = true).
+// Bijective XCD-grouping of workgroup ids (cdna_hip_programming.md T1): the
+// dispatcher deals ids round-robin over the 8 XCDs, so give XCD x the
+// contiguous id range [start(x), start(x+1)).
+__device__ __forceinline__ uint32_t xcd_group(uint32_t b, uint32_t n) {
+  const uint32_t q = n / 8, r = n % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// One workgroup of WG threads per tile (PIPE = false), or a persistent grid
+// that walks the tiles and issues the loads of its next tile before
+// computing the current one (PIPE = true).
 template <int K, int R, bool ACC, int CPT, bool NT, bool BRANCHY, bool COPY, bool PIPE, bool LDS,
-          int WAVES>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
+          int WAVES, int WG, bool XMAP>
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 gf8_apply(const Gf8Args<K, R> a) {
-  constexpr uint32_t TB = kTileBytes * CPT;
+  constexpr uint32_t CS = (uint32_t)WG * 16u;  // bytes of one column group
+  constexpr uint32_t TB = CS * CPT;
   __shared__ Gf8Lds<K, R> lds;
   if (LDS) {
-    for (uint32_t i = threadIdx.x; i < (uint32_t)(R * K); i += kThreads) {
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(R * K); i += WG) {
       const uint32_t* t = a.tab[i / K][i % K];
       lds.t[i][0] = u32x4{t[0], t[1], t[2], t[3]};
       lds.t[i][1] = u32x4{t[4], 0u, 0u, 0u};
@@ -291,17 +306,18 @@ gf8_apply(const Gf8Args<K, R> a) {
     __syncthreads();
   }
   if (!PIPE) {
-    const uint32_t obj = blockIdx.x / a.tiles;
-    const uint32_t tile = blockIdx.x - obj * a.tiles;
+    const uint32_t b = XMAP ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t obj = b / a.tiles;
+    const uint32_t tile = b - obj * a.tiles;
     const uint32_t t0 = tile * TB;
     const uint32_t off = t0 + threadIdx.x * 16u;
     const bool full = t0 + TB <= a.vmin;  // wave-uniform
     u32x4 d[CPT][K];
-    gf8_load<K, R, CPT, NT>(a, obj, off, full, d);
+    gf8_load<K, R, CPT, NT, CS>(a, obj, off, full, d);
     u32x4 acc[CPT][R];
-    gf8_init_store<K, R, ACC, CPT, NT>(a, obj, off, acc);
+    gf8_init_store<K, R, ACC, CPT, NT, CS>(a, obj, off, acc);
     gf8_tile<K, R, CPT, BRANCHY, COPY, LDS>(a, lds, d, acc);
-    gf8_store<K, R, CPT, NT>(a, obj, off, full, acc);
+    gf8_store<K, R, CPT, NT, CS>(a, obj, off, full, acc);
     return;
   }
   const uint32_t total = a.total_tiles;
@@ -311,7 +327,7 @@ gf8_apply(const Gf8Args<K, R> a) {
   uint32_t obj = g / a.tiles;
   uint32_t t0 = (g - obj * a.tiles) * TB;
   bool full = t0 + TB <= a.vmin;
-  gf8_load<K, R, CPT, NT>(a, obj, t0 + threadIdx.x * 16u, full, nxt);
+  gf8_load<K, R, CPT, NT, CS>(a, obj, t0 + threadIdx.x * 16u, full, nxt);
   while (true) {
     u32x4 d[CPT][K];
 #pragma unroll
@@ -326,12 +342,12 @@ gf8_apply(const Gf8Args<K, R> a) {
       obj = g / a.tiles;
       t0 = (g - obj * a.tiles) * TB;
       full = t0 + TB <= a.vmin;
-      gf8_load<K, R, CPT, NT>(a, obj, t0 + threadIdx.x * 16u, full, nxt);
+      gf8_load<K, R, CPT, NT, CS>(a, obj, t0 + threadIdx.x * 16u, full, nxt);
     }
     u32x4 acc[CPT][R];
-    gf8_init_store<K, R, ACC, CPT, NT>(a, cobj, coff, acc);
+    gf8_init_store<K, R, ACC, CPT, NT, CS>(a, cobj, coff, acc);
     gf8_tile<K, R, CPT, BRANCHY, COPY, LDS>(a, lds, d, acc);
-    gf8_store<K, R, CPT, NT>(a, cobj, coff, cfull, acc);
+    gf8_store<K, R, CPT, NT, CS>(a, cobj, coff, cfull, acc);
     if (!more) break;
   }
 }
@@ -664,7 +680,8 @@ int device_cus();  // compute units of the current device (kernels.hip)
 // when enough coefficients are 0/1, the paired all-table form otherwise).
 template <int K, int R, bool ACC, int CPT = kGf8Default.cpt, bool NT = kGf8Default.nt,
           int BRANCHY = kGf8Default.branchy, bool COPY = kGf8Default.copy, bool PIPE = false,
-          bool LDS = kGf8Default.lds, int WAVES = kGf8Default.waves>
+          bool LDS = kGf8Default.lds, int WAVES = kGf8Default.waves, int WG = kThreads,
+          bool XMAP = false>
 int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   Gf8Args<K, R> a;
   a.one = a.zero = 0;
@@ -685,7 +702,7 @@ int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
       n01 += cf <= 1;
     }
   }
-  const uint32_t tb = kTileBytes * CPT;
+  const uint32_t tb = (uint32_t)WG * 16u * CPT;
   a.tiles = (uint32_t)((p.block_size + tb - 1) / tb);
   a.vmin = vmin;
   a.total_tiles = (uint32_t)(c.no * a.tiles);
@@ -699,11 +716,11 @@ int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
     grid = grid < cap ? grid : cap;
   }
   if (branchy)
-    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, true, COPY, PIPE, LDS, WAVES>), dim3(grid),
-                       dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, true, COPY, PIPE, LDS, WAVES, WG, XMAP>),
+                       dim3(grid), dim3(WG), 0, s, a);
   else
-    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, false, COPY, PIPE, LDS, WAVES>), dim3(grid),
-                       dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, false, COPY, PIPE, LDS, WAVES, WG, XMAP>),
+                       dim3(grid), dim3(WG), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }
 

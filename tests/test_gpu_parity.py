@@ -20,6 +20,10 @@ CONFIGS = [
     ("cauchyrs", 4, 2, 3), ("cauchyrs", 10, 4, 8), ("cauchyrs", 10, 4, 10), ("cauchyrs", 6, 3, 4),
     ("liberation", 4, 2, 7), ("liberation", 5, 2, 5), ("liberation", 10, 2, 11),
     ("liberation", 4, 2, 5),
+    # chunked launches: >16 inputs (accumulating launches), >4 outputs,
+    # cauchyrs beyond the bitsliced kernel's w <= 16 (masked bitmatrix kernel)
+    ("vandrs", 20, 6, 8), ("isars", 18, 5, 8), ("cauchyrs", 5, 3, 17), ("liberation", 3, 2, 31),
+    ("vandrs", 17, 3, 16),
 ]
 
 

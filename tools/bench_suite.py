@@ -16,19 +16,22 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 PEAK = 8000.0
 
 
-def timed(torch, fn, reps):
+def timed(torch, fn, reps, warmup=10):
+    """Median launch time with the launches back to back on one stream (as in
+    bench.py), after `warmup` untimed launches (DVFS settles)."""
     stream = torch.cuda.current_stream()
-    fn()
+    for _ in range(warmup):
+        fn()
     torch.cuda.synchronize()
-    ts = []
+    evs = []
     for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
         fn()
         b.record(stream)
-        torch.cuda.synchronize()
-        ts.append(a.elapsed_time(b))
-    return statistics.median(ts)
+        evs.append((a, b))
+    torch.cuda.synchronize()
+    return statistics.median(a.elapsed_time(b) for a, b in evs)
 
 
 def row(name, op, ms, alg, payload, extra=None):
@@ -83,7 +86,7 @@ def stripe_case(torch, le, cls, k, m, w, size, n, reps, erased, repair_ids, name
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--skip-cpu", action="store_true")
     args = ap.parse_args()

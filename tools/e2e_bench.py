@@ -41,6 +41,35 @@ def main():
     print(json.dumps({"path": "nif leoec_encode, pageable, 1 object/call, 1 thread",
                       "GiBps": round(n * size / t / 2**30, 2), "us_per_object": round(t / n * 1e6, 1)}))
 
+    # --- C ABI leoec_encode (host memory), T concurrent callers (dirty schedulers)
+    import threading
+    bsz = (K + M - filled) * bs
+    for T in (1, 4, 8, 16):
+        per = 64
+        srcs = [np.random.default_rng(t).integers(0, 256, size, dtype=np.uint8) for t in range(T)]
+        outs = [np.empty(bsz, dtype=np.uint8) for _ in range(T)]
+
+        def work(t):
+            for _ in range(per):
+                rc = le.lib.leoec_encode(2, K, M, W, srcs[t].ctypes.data, size, outs[t].ctypes.data, bsz)
+                assert rc == 0
+
+        for t in range(T):  # warm each thread's stream / staging
+            work_t = threading.Thread(target=lambda: le.lib.leoec_encode(
+                2, K, M, W, srcs[0].ctypes.data, size, outs[0].ctypes.data, bsz))
+            work_t.start()
+            work_t.join()
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        t = time.perf_counter() - t0
+        print(json.dumps({"path": f"C ABI leoec_encode, pageable 1 MiB objects, {T} caller threads",
+                          "GiBps": round(T * per * size / t / 2**30, 2),
+                          "us_per_object_per_thread": round(t / per * 1e6, 1)}))
+
     # --- pinned, batched, two streams
     total, chunk = 1024, 64
     host = torch.randint(0, 256, (total, size), dtype=torch.uint8).pin_memory()
