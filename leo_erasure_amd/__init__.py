@@ -12,11 +12,12 @@ from .api import (  # noqa: F401
     CODING_CLASS_CAUCHYRS, CODING_CLASS_ISA_VANDRS, CODING_CLASS_LIBERATION,
     CODING_CLASS_VANDRS, DEF_CODING_CLASS, DEF_CODING_PARAMS, decode, encode,
     env_default_coder, gf_init, layout, nif_decode, nif_encode, nif_repair, repair,
-    set_default_coder,
+    set_default_coder, write_blocks, encode_file, decode_file,
 )
 from . import device  # noqa: F401
 
 __all__ = [
     "encode", "decode", "repair", "gf_init", "layout", "nif_encode", "nif_decode", "nif_repair",
     "set_default_coder", "env_default_coder", "device", "LeoecError", "version",
+    "write_blocks", "encode_file", "decode_file",
 ]

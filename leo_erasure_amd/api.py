@@ -293,3 +293,62 @@ def repair(*args):
     if len(args) == 5:
         return nif_repair(*args)
     raise TypeError("repair/%d is undefined" % len(args))
+
+
+# ---------------------------------------------------------------------------
+# File helpers of src/leo_erasure.erl:63-136,255-279 (blocks/<File>.<Id>).
+BLOCKSTOR = "blocks/"
+
+
+def write_blocks(file_name, blocks, cnt):
+    """write_blocks/3: blocks/<FileName>.<Cnt>, Cnt counting up; returns the next Cnt."""
+    os.makedirs(BLOCKSTOR, exist_ok=True)
+    for b in blocks:
+        with open(os.path.join(BLOCKSTOR, "%s.%d" % (file_name, cnt)), "wb") as fh:
+            fh.write(b)
+        cnt += 1
+    return cnt
+
+
+def encode_file(*args):
+    """encode_file/1, encode_file/3 (src/leo_erasure.erl:63-96)."""
+    if len(args) == 1:
+        return encode_file(env_default_coder(), DEF_CODING_PARAMS, args[0])
+    coding_class, params, file_name = args
+    try:
+        with open(file_name, "rb") as fh:
+            data = fh.read()
+    except OSError as e:
+        return _err(e.strerror)
+    res = nif_encode(coding_class, params, data, len(data))
+    if res[0] != "ok":
+        return res
+    return write_blocks(file_name, res[1], 0)
+
+
+def _check_available_blocks(file_name, cnt):
+    """check_available_blocks/3: ids cnt..0 present on disk, ascending."""
+    avail = []
+    for i in range(cnt, -1, -1):
+        if os.path.isfile(os.path.join(BLOCKSTOR, "%s.%d" % (file_name, i))):
+            avail.insert(0, i)
+    return avail
+
+
+def decode_file(*args):
+    """decode_file/2, decode_file/4 (src/leo_erasure.erl:102-136): reads the
+    blocks of ids 14..0 present on disk (as the reference does) and writes
+    <FileName>.dec."""
+    if len(args) == 2:
+        return decode_file(env_default_coder(), DEF_CODING_PARAMS, args[0], args[1])
+    coding_class, params, file_name, obj_size = args
+    id_with_block = []
+    for i in _check_available_blocks(file_name, 14):  # read_blocks/3 builds the list reversed
+        with open(os.path.join(BLOCKSTOR, "%s.%d" % (file_name, i)), "rb") as fh:
+            id_with_block.insert(0, (i, fh.read()))
+    res = decode(coding_class, params, id_with_block, obj_size)
+    if res[0] != "ok":
+        return res
+    with open(file_name + ".dec", "wb") as fh:
+        fh.write(res[1])
+    return "ok"

@@ -285,3 +285,16 @@ def test_golden_fixtures_gpu(gpu, le):
         st, blocks = le.nif_encode(ent["class"], (ent["k"], ent["m"], ent["w"]),
                                    z["data"].tobytes(), ent["size"])
         assert st == "ok" and b"".join(blocks) == z["blocks"].tobytes(), ent["file"]
+
+
+def test_file_helpers(gpu, le, tmp_path, monkeypatch):
+    """file_test (test/leo_erasure_tests.erl:98-116): encode_file, delete blocks
+    0/2/4/6, decode_file, compare."""
+    monkeypatch.chdir(tmp_path)
+    data = rand_bytes(10485760 + 1, 98)
+    (tmp_path / "testbin").write_bytes(data)
+    assert le.encode_file("vandrs", (10, 4, 8), "testbin") == 14
+    for i in (0, 2, 4, 6):
+        (tmp_path / "blocks" / ("testbin.%d" % i)).unlink()
+    assert le.decode_file("vandrs", (10, 4, 8), "testbin", len(data)) == "ok"
+    assert (tmp_path / "testbin.dec").read_bytes() == data
