@@ -24,6 +24,21 @@ ChunkFn gf8_pick(std::index_sequence<I...>, int k, int r, bool acc) {
   return sel[k - 1](r, acc);
 }
 
+ChunkFn gf16_pick(int r, bool acc) {
+  static const ChunkFn tbl[2][kMaxR] = {
+      {&launch_gf16_t<1, false>, &launch_gf16_t<2, false>, &launch_gf16_t<3, false>,
+       &launch_gf16_t<4, false>},
+      {&launch_gf16_t<1, true>, &launch_gf16_t<2, true>, &launch_gf16_t<3, true>,
+       &launch_gf16_t<4, true>}};
+  return tbl[acc ? 1 : 0][r - 1];
+}
+
+// LEOEC_GF16_SHIFT=1 selects the shift-and-add kernel for w = 16 (A/B).
+int gf16_pick_env() {
+  const char* e = std::getenv("LEOEC_GF16_SHIFT");
+  return e ? std::atoi(e) : 0;
+}
+
 template <int W>
 ChunkFn gfw_pick(int r, bool acc) {
   static const ChunkFn tbl[2][kMaxR] = {
@@ -82,7 +97,7 @@ int launch(const GfApply& p, hipStream_t s) {
             if (var > 0 && gf8_variant(var)) fn = gf8_variant(var);
           }
         } else if (p.w == 16) {
-          fn = gfw_pick<16>(nr, j0 > 0);
+          fn = gf16_pick_env() ? gfw_pick<16>(nr, j0 > 0) : gf16_pick(nr, j0 > 0);
         } else {
           fn = gfw_pick<32>(nr, j0 > 0);
         }

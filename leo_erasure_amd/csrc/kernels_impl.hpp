@@ -420,6 +420,88 @@ __global__ void __launch_bounds__(kThreads) gfw_apply(const GfwArgs<R> a) {
 }
 
 // ===========================================================================
+// GF(2^16) with v_perm over 2-bit fields.  A dword holds two little-endian
+// words; for field f (bits 2f, 2f+1 of each word) one v_perm returns both
+// 16-bit products c*(v << 2f) at once: selector bytes [v0, v0|4, v1, v1|4]
+// pick the low byte of the product from a 4-entry table in src1 and the
+// high byte from one in src0.  8 perms + 4 xor3 per coefficient per dword;
+// the 8 selector dwords of an input dword are shared by every row.  Tables
+// (R x K coefficients x 8 fields x 2 dwords) are built in LDS by the block.
+template <int R>
+struct Gf16Args {
+  DevShard in[kMaxK];
+  DevShard out[R];
+  uint32_t coef[R][kMaxK];
+  int K;
+  uint32_t tiles;
+  uint32_t vmin;
+};
+
+__device__ __forceinline__ uint32_t gf16_x2(uint32_t v) {  // v * x mod 0x1100B
+  return ((v << 1) ^ ((v & 0x8000u) ? 0x1100Bu : 0u)) & 0xFFFFu;
+}
+
+template <int R, bool ACC>
+__global__ void __launch_bounds__(kThreads) gf16_apply(const Gf16Args<R> a) {
+  __shared__ uint32_t tab[R * kMaxK][8][2];
+  const int K = a.K;
+  for (int i = threadIdx.x; i < R * K * 8; i += kThreads) {
+    const int ci = i >> 3, f = i & 7;
+    uint32_t d1 = a.coef[ci / K][ci % K] & 0xFFFFu;
+    for (int t = 0; t < 2 * f; ++t) d1 = gf16_x2(d1);
+    const uint32_t d2 = gf16_x2(d1), d3 = d1 ^ d2;
+    tab[ci][f][0] = ((d1 & 0xFFu) << 8) | ((d2 & 0xFFu) << 16) | ((d3 & 0xFFu) << 24);
+    tab[ci][f][1] = ((d1 >> 8) << 8) | ((d2 >> 8) << 16) | ((d3 >> 8) << 24);
+  }
+  __syncthreads();
+  const uint32_t obj = blockIdx.x / a.tiles;
+  const uint32_t tile = blockIdx.x - obj * a.tiles;
+  const uint32_t t0 = tile * kTileBytes;
+  const uint32_t off = t0 + threadIdx.x * 16u;
+  const bool full = t0 + kTileBytes <= a.vmin;
+  const uint64_t o = obj;
+  u32x4 acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    acc[r] = u32x4{0u, 0u, 0u, 0u};
+    if (ACC) acc[r] = load_guarded(a.out[r].base + o * a.out[r].stride, off, a.out[r].valid);
+  }
+  for (int j = 0; j < K; ++j) {
+    const uint8_t* p = a.in[j].base + o * a.in[j].stride;
+    const u32x4 x = full ? ld16<true>(p + off) : load_guarded(p, off, a.in[j].valid);
+    uint32_t sel[8][4];
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t t = (x[e] >> (2 * f)) & 0x00030003u;
+        sel[f][e] = (t << 8) | t | 0x04000400u;
+      }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t(*tb)[2] = tab[r * K + j];
+#pragma unroll
+      for (int f = 0; f < 8; f += 2) {
+        const uint32_t l0 = tb[f][0], h0 = tb[f][1], l1 = tb[f + 1][0], h1 = tb[f + 1][1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc[r][e] = xor3(acc[r][e], perm(h0, l0, sel[f][e]), perm(h1, l1, sel[f + 1][e]));
+      }
+    }
+  }
+  if (full) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      st16<true>(const_cast<uint8_t*>(a.out[r].base) + o * a.out[r].stride + off, acc[r]);
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      store_guarded(const_cast<uint8_t*>(a.out[r].base) + o * a.out[r].stride, off,
+                    a.out[r].valid, acc[r]);
+  }
+}
+
+// ===========================================================================
 // Bitmatrix (GF(2)) over packets of ps bytes.
 struct BitArgs {
   DevShard in[kMaxK];
@@ -743,6 +825,28 @@ int launch_gfw_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   a.vmin = vmin;
   hipLaunchKernelGGL((gfw_apply<W, R, ACC>), dim3((uint32_t)(c.no * c.tiles)), dim3(kThreads), 0,
                      s, a);
+  return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
+}
+
+template <int R, bool ACC>
+int launch_gf16_t(const GfApply& p, const Chunk& c, hipStream_t s) {
+  Gf16Args<R> a;
+  uint32_t vmin = 0xFFFFFFFFu;
+  a.K = c.nk;
+  for (int j = 0; j < kMaxK; ++j) {
+    a.in[j] = j < c.nk ? dev_shard(p.in[c.j0 + j], c.o0) : DevShard{nullptr, 0, 0, 0};
+    if (j < c.nk) vmin = a.in[j].valid < vmin ? a.in[j].valid : vmin;
+  }
+  for (int r = 0; r < R; ++r) {
+    a.out[r] = dev_shard(p.out[c.r0 + r], c.o0);
+    vmin = a.out[r].valid < vmin ? a.out[r].valid : vmin;
+    for (int j = 0; j < kMaxK; ++j)
+      a.coef[r][j] = j < c.nk ? p.coef[(size_t)(c.r0 + r) * p.K + c.j0 + j] : 0u;
+  }
+  a.tiles = c.tiles;
+  a.vmin = vmin;
+  hipLaunchKernelGGL((gf16_apply<R, ACC>), dim3((uint32_t)(c.no * c.tiles)), dim3(kThreads), 0, s,
+                     a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }
 

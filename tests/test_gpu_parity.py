@@ -298,3 +298,16 @@ def test_file_helpers(gpu, le, tmp_path, monkeypatch):
         (tmp_path / "blocks" / ("testbin.%d" % i)).unlink()
     assert le.decode_file("vandrs", (10, 4, 8), "testbin", len(data)) == "ok"
     assert (tmp_path / "testbin.dec").read_bytes() == data
+
+
+@pytest.mark.parametrize("shift", ["0", "1"])
+def test_gf16_kernel_forms_agree(gpu, le, oracle, shift, monkeypatch):
+    """w = 16 through the v_perm kernel and the shift-and-add kernel."""
+    monkeypatch.setenv("LEOEC_GF16_SHIFT", shift)
+    for k, m in [(10, 4), (4, 2), (17, 5)]:
+        data = rand_bytes(200011, k * m)
+        st, blocks = le.nif_encode("vandrs", (k, m, 16), data, len(data))
+        assert st == "ok" and blocks == oracle.encode("vandrs", k, m, 16, data)
+        ids = list(range(m, k + m))
+        st, out = le.nif_decode("vandrs", (k, m, 16), [blocks[i] for i in ids], ids, len(data))
+        assert st == "ok" and out == data
