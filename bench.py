@@ -76,7 +76,8 @@ def cpu_baseline(size, target_s, threads, sample_objs=2048):
     gib = 2 * n * passes * size / (te + td) / 2**30
     return {
         "value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-        "simd": {0: "scalar", 2: "avx2-pshufb"}.get(O.simd_level(), "scalar"),
+        "simd": {0: "scalar", 2: "avx2-pshufb (ISA-L split tables)",
+                 3: "avx512-gfni (ISA-L gf2p8affine)"}.get(O.simd_level(), "scalar"),
         "sample": f"{passes} passes over {n} x {size} B objects: vandrs RS({K},{M},8) encode "
                   f"{te:.2f} s + in-place decode of data blocks {ERASED} {td:.2f} s, "
                   f"{threads} threads",

@@ -700,9 +700,27 @@ int orc_repair(int coding, int k, int m, int w, const uint8_t *const *blocks, co
 int orc_simd_level(void) {
 #if defined(__x86_64__)
   __builtin_cpu_init();
+  if (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+      __builtin_cpu_supports("gfni"))
+    return 3;
   if (__builtin_cpu_supports("avx2")) return 2;
 #endif
   return 0;
+}
+
+/* ISA-L's AVX-512 + GFNI technique (ec_encode_data_avx512_gfni): multiply by
+ * c is an 8x8 GF(2) matrix applied to every byte by vgf2p8affineqb; row i of
+ * the matrix (output bit i) is byte 7-i of the qword. */
+static uint64_t gfni_matrix(uint32_t c) {
+  pthread_once(&g8once, g8init);
+  uint64_t A = 0;
+  for (int i = 0; i < 8; i++) {
+    uint64_t row = 0;
+    for (int j = 0; j < 8; j++)
+      if ((g8mul[c][1 << j] >> i) & 1) row |= 1ull << j;
+    A |= row << (8 * (7 - i));
+  }
+  return A;
 }
 
 static void init_tables(int nrow, int ncol, const uint32_t *rows, uint8_t *tbl) {
@@ -761,6 +779,32 @@ __attribute__((target("avx2"))) static void apply_avx2(int nin, int nout, const 
 }
 #endif
 
+#if defined(__x86_64__)
+__attribute__((target("avx512f,avx512bw,gfni"))) static void apply_gfni(
+    int nin, int nout, const uint64_t *mats, const uint8_t *tbl, const uint8_t *const *in,
+    uint8_t *const *out, uint64_t len) {
+  uint64_t i = 0;
+  for (; i + 64 <= len; i += 64) {
+    __m512i acc[16];
+    for (int o = 0; o < nout; o++) acc[o] = _mm512_setzero_si512();
+    for (int j = 0; j < nin; j++) {
+      const __m512i x = _mm512_loadu_si512((const void *)(in[j] + i));
+      for (int o = 0; o < nout; o++)
+        acc[o] = _mm512_xor_si512(
+            acc[o], _mm512_gf2p8affine_epi64_epi8(x, _mm512_set1_epi64((long long)mats[o * nin + j]), 0));
+    }
+    for (int o = 0; o < nout; o++) _mm512_storeu_si512((void *)(out[o] + i), acc[o]);
+  }
+  if (i < len) {
+    const uint8_t *in2[256];
+    uint8_t *out2[256];
+    for (int j = 0; j < nin; j++) in2[j] = in[j] + i;
+    for (int o = 0; o < nout; o++) out2[o] = out[o] + i;
+    apply_scalar(nin, nout, tbl, in2, out2, len - i);
+  }
+}
+#endif
+
 typedef struct {
   int op, k, m, nout, simd;
   const uint8_t *objs;
@@ -768,6 +812,7 @@ typedef struct {
   int o0, o1;
   uint8_t *parity;
   const uint8_t *tbl;
+  const uint64_t *mats; /* GFNI affine matrices, nout x k */
   const int *want;      /* decode: erased data ids */
   const int *surv;      /* decode: survivor ids */
 } bench_job;
@@ -805,7 +850,8 @@ static void *bench_worker(void *arg) {
       for (int i = 0; i < J->nout; i++) out[i] = (uint8_t *)blk[J->want[i]];
     }
 #if defined(__x86_64__)
-    if (J->simd >= 2) apply_avx2(nin, J->nout, J->tbl, in, out, bs);
+    if (J->simd >= 3) apply_gfni(nin, J->nout, J->mats, J->tbl, in, out, bs);
+    else if (J->simd >= 2) apply_avx2(nin, J->nout, J->tbl, in, out, bs);
     else
 #endif
       apply_scalar(nin, J->nout, J->tbl, in, out, bs);
@@ -839,22 +885,26 @@ int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride
     if (rc) goto done;
   }
   init_tables(nout, k, rows, tbl);
+  uint64_t *mats = malloc(sizeof(uint64_t) * (size_t)nout * k);
+  for (int i = 0; i < nout * k; i++) mats[i] = gfni_matrix(rows[i]);
   {
     pthread_t th[256];
     bench_job jobs[256];
     if (threads > 256) threads = 256;
     int simd = force_scalar ? 0 : orc_simd_level();
+    if (force_scalar > 1) simd = force_scalar;  /* 2: force avx2, 3: force gfni */
     for (int t = 0; t < threads; t++) {
       bench_job *J = &jobs[t];
       J->op = op; J->k = k; J->m = m; J->nout = nout; J->simd = simd;
       J->objs = objs; J->stride = obj_stride; J->size = size; J->bs = bs;
       J->o0 = (int)((long long)nobj * t / threads);
       J->o1 = (int)((long long)nobj * (t + 1) / threads);
-      J->parity = parity; J->tbl = tbl; J->want = erased; J->surv = surv;
+      J->parity = parity; J->tbl = tbl; J->mats = mats; J->want = erased; J->surv = surv;
       pthread_create(&th[t], NULL, bench_worker, J);
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
   }
+  free(mats);
 done:
   free(C); free(rows); free(tbl);
   return rc;

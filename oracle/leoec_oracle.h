@@ -101,7 +101,7 @@ int orc_repair(int coding, int k, int m, int w, const uint8_t *const *blocks,
 int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride,
                   uint64_t size, int nobj, uint8_t *parity, const int *erased,
                   int nerased, int threads, int force_scalar);
-int orc_simd_level(void);   /* 0 scalar, 2 avx2 */
+int orc_simd_level(void);   /* 0 scalar, 2 avx2 (PSHUFB), 3 avx512bw+gfni (affine) */
 
 #ifdef __cplusplus
 }
