@@ -58,14 +58,29 @@ def _err(reason):
 
 
 def _as_bytes(x):
+    """enif_inspect_iolist_as_binary: a binary, or a (nested) list of binaries
+    and bytes 0..255.  Tuples and out-of-range integers are not iolists."""
     if isinstance(x, (bytes, bytearray, memoryview)):
         return bytes(x)
-    if isinstance(x, (list, tuple)):  # iolist
-        try:
-            return b"".join(_as_bytes(p) if not isinstance(p, int) else bytes([p]) for p in x)
-        except (TypeError, ValueError):
-            return None
-    return None
+    if not isinstance(x, list):
+        return None
+    out = bytearray()
+    for p in x:
+        if isinstance(p, int) and not isinstance(p, bool):
+            if not 0 <= p <= 255:
+                return None
+            out.append(p)
+        else:
+            b = _as_bytes(p)
+            if b is None:
+                return None
+            out += b
+    return bytes(out)
+
+
+def _c_int(v):
+    """enif_get_int: an integer that fits a C int."""
+    return isinstance(v, int) and not isinstance(v, bool) and -(1 << 31) <= v < (1 << 31)
 
 
 def _coding_params(params):
@@ -75,7 +90,7 @@ def _coding_params(params):
     names = ("Invalid K", "Invalid M", "Invalid W")
     vals = []
     for i in range(3):
-        if i >= len(params) or not isinstance(params[i], int) or isinstance(params[i], bool):
+        if i >= len(params) or not _c_int(params[i]):
             return None, names[i]
         vals.append(params[i])
     return tuple(vals), None
@@ -154,7 +169,7 @@ def _parse_blocks(block_list, id_list):
         bb = _as_bytes(b)
         if bb is None:
             return None, None, "Invalid Block"
-        if not isinstance(i, int) or isinstance(i, bool):
+        if not _c_int(i):
             return None, None, "Invalid ID"
         blocks.append(bb)
         ids.append(i)
@@ -204,7 +219,7 @@ def nif_repair(coding_class, params, block_list, id_list, repair_id_list):
     if not isinstance(repair_id_list, list):
         return _err("Repair ID List Needed")
     for r in repair_id_list:
-        if not isinstance(r, int) or isinstance(r, bool):
+        if not _c_int(r):
             return _err("Invalid Repair ID")
     if not isinstance(coding_class, str):
         return _err("Expect coding")

@@ -11,8 +11,9 @@
 // round trip never blocks a normal scheduler thread.
 //
 // Built only where erl_nif.h exists:
-//   c++ -O2 -fPIC -shared -DHAVE_ERL_NIF -I$ERL_ROOT/usr/include -I<repo>/include \
+//   c++ -O2 -fPIC -shared -DHAVE_ERL_NIF -I$ERL_ROOT/usr/include -I<repo>/include
 //       leo_erasure_nif.cpp -L<repo>/leo_erasure_amd -lleoec -o priv/leo_erasure.so
+// tests/nif_harness/ compiles this file against a test-double erl_nif.h.
 #ifdef HAVE_ERL_NIF
 #include <erl_nif.h>
 
