@@ -259,9 +259,11 @@ def test_gpu_engine_errors_through_shim(nif, gpu, le):
     # fewer than k blocks
     assert err(nif.call("decode", VANDRS, PARAMS, blocks[:9], list(range(9)), len(DATA))) == \
         le.strerror(-9)
-    # duplicate ids
+    # duplicate ids: fewer than k distinct -> not enough; k distinct + a repeat -> not unique
     ids = list(range(9)) + [0]
-    assert err(nif.call("decode", VANDRS, PARAMS, blocks[:10], ids, len(DATA))) == le.strerror(-10)
+    assert err(nif.call("decode", VANDRS, PARAMS, blocks[:10], ids, len(DATA))) == le.strerror(-9)
+    ids = list(range(10)) + [0]
+    assert err(nif.call("decode", VANDRS, PARAMS, blocks[:11], ids, len(DATA))) == le.strerror(-10)
     # id out of range
     ids = list(range(9)) + [14]
     assert err(nif.call("decode", VANDRS, PARAMS, blocks[:10], ids, len(DATA))) == \
