@@ -16,13 +16,17 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 PEAK = 8000.0
 
 
-def timed(torch, fn, reps, warmup=10):
+def timed(torch, fn, reps, warmup_s=0.2):
     """Median launch time with the launches back to back on one stream (as in
-    bench.py), after `warmup` untimed launches (DVFS settles)."""
+    bench.py), after at least `warmup_s` seconds of untimed launches: a short
+    warmup after an idle gap (allocation, verification) measures the GPU
+    still ramping its clocks — the first op of a config read ~12 % low."""
     stream = torch.cuda.current_stream()
-    for _ in range(warmup):
-        fn()
-    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < warmup_s:
+        for _ in range(10):
+            fn()
+        torch.cuda.synchronize()
     evs = []
     for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -44,43 +48,54 @@ def row(name, op, ms, alg, payload, extra=None):
     return r
 
 
-def stripe_case(torch, le, cls, k, m, w, size, n, reps, erased, repair_ids, name, verify=True):
-    """Objects stored as full stripes [n][(k+m)*bs]: data blocks then coding
-    blocks, so encode / decode / repair all run on one buffer."""
+def stripe_case(torch, le, cls, k, m, w, size, n, reps, erased, repair_ids, name, verify=True,
+                layout="object"):
+    """layout "object" (bench.py's): objects at a k*bs row stride (zero pad after
+    `size`), parity in its own buffer at the same row stride (leoec_repair_dev takes one
+    stride for all k+m blocks).  layout "stripe": full stripes [n][(k+m)*bs],
+    data blocks then coding blocks in one row — parity written next to the
+    data it is read from, which costs HBM efficiency (tools/layout_exp.py)."""
     bs, _ = le.layout(cls, (k, m, w), size)
-    stride = (k + m) * bs
     g = torch.Generator(device="cuda").manual_seed(0x1E0E)
-    stripe = torch.zeros((n, stride), dtype=torch.uint8, device="cuda")
-    stripe[:, :size] = torch.randint(0, 256, (n, size), dtype=torch.uint8, device="cuda", generator=g)
-    objs = stripe
-    parity = stripe[:, k * bs:]
-    ref = stripe[:, :size].clone()
+    if layout == "stripe":
+        stride = (k + m) * bs
+        buf = torch.zeros((n, stride), dtype=torch.uint8, device="cuda")
+        objs, parity = buf, buf[:, k * bs:]
+    else:
+        stride = max(k, m) * bs  # >= size; the tail block's zero pad lies inside the row
+        objs = torch.zeros((n, stride), dtype=torch.uint8, device="cuda")
+        parity = torch.zeros((n, stride), dtype=torch.uint8, device="cuda")
+    objs[:, :size] = torch.randint(0, 256, (n, size), dtype=torch.uint8, device="cuda", generator=g)
+    ref = objs[:, :size].clone()
+    extra = {"layout": layout}
     enc = lambda: le.device.encode(cls, (k, m, w), objs, size, parity)  # noqa: E731
     t_enc = timed(torch, enc, reps)
     out = []
-    out.append(row(name, "encode", t_enc, (k + m) * bs * n, size * n))
+    out.append(row(name, "encode", t_enc, (k + m) * bs * n, size * n, extra))
     if erased:
         dec = lambda: le.device.decode(cls, (k, m, w), objs, size, parity, erased)  # noqa: E731
         t_dec = timed(torch, dec, reps)
         e = len([x for x in erased if x < k])
-        out.append(row(name, "decode%s" % erased, t_dec, (k + e) * bs * n, size * n))
+        out.append(row(name, "decode%s" % erased, t_dec, (k + e) * bs * n, size * n, extra))
         out.append(row(name, "encode+decode", t_enc + t_dec, (2 * k + m + e) * bs * n,
-                       2 * size * n))
+                       2 * size * n, extra))
         if verify:
-            stripe[:, :size][:, :e * bs] = 0
+            objs[:, :e * bs] = 0
             dec()
             torch.cuda.synchronize()
-            assert torch.equal(stripe[:, :size], ref), f"{name}: decode mismatch"
+            assert torch.equal(objs[:, :size], ref), f"{name}: decode mismatch"
     if repair_ids:
-        blocks = [None if b in repair_ids else stripe[:, b * bs:] for b in range(k + m)]
+        def blk(b):
+            return objs[:, b * bs:] if b < k else parity[:, (b - k) * bs:]
+        blocks = [None if b in repair_ids else blk(b) for b in range(k + m)]
         outs = [torch.empty((n, bs), dtype=torch.uint8, device="cuda") for _ in repair_ids]
         rep = lambda: le.device.repair(cls, (k, m, w), blocks, bs, repair_ids, outs, n)  # noqa
         t_rep = timed(torch, rep, reps)
         out.append(row(name, "repair%s" % repair_ids, t_rep, (k + len(repair_ids)) * bs * n,
-                       len(repair_ids) * bs * n))
+                       len(repair_ids) * bs * n, extra))
         if verify:
             for i, b in enumerate(repair_ids):
-                assert torch.equal(outs[i], stripe[:, b * bs:(b + 1) * bs]), f"{name}: repair {b}"
+                assert torch.equal(outs[i], blk(b)[:, :bs]), f"{name}: repair {b}"
     return out
 
 
@@ -101,6 +116,8 @@ def main():
                 "cfg0: vandrs RS(4,2,8) 1 MiB x1024 (GPU)")
     stripe_case(torch, le, "vandrs", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], [0, 5, 10, 13],
                 "cfg1/2: vandrs RS(10,4,8) 1 MiB x1024")
+    stripe_case(torch, le, "vandrs", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], [0, 5, 10, 13],
+                "cfg1/2: vandrs RS(10,4,8) 1 MiB x1024", layout="stripe")
     stripe_case(torch, le, "cauchyrs", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], [0, 5, 10, 13],
                 "cfg3: cauchyrs(10,4,8) bitmatrix 1 MiB x1024")
     for env, label in [({"LEOEC_GFBIT_LW": "1"}, "lane 4 B"), ({"LEOEC_GFBIT_LW": "4"}, "lane 16 B"),

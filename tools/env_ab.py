@@ -1,0 +1,105 @@
+"""A/B of kernel-selection environment variables on one config, interleaved
+rounds in one process (the engine reads its LEOEC_* knobs per launch).
+
+    python tools/env_ab.py --coding cauchyrs --k 10 --m 4 --w 8 \\
+        --variants "LEOEC_GFBIT_PF=1;LEOEC_GFBIT_PF=0;LEOEC_GFBIT_LW=1"
+
+Each variant is `;`-separated, its settings `,`-separated (empty = defaults).
+Objects are laid out as in bench.py's family (object rows, separate parity),
+after a >=0.3 s time-based warmup per variant.  Output: one JSON line per
+(variant, op) with the median over rounds of the median launch time.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--coding", default="cauchyrs")
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--m", type=int, default=4)
+    ap.add_argument("--w", type=int, default=8)
+    ap.add_argument("--size", type=int, default=1 << 20)
+    ap.add_argument("--objects", type=int, default=1024)
+    ap.add_argument("--erased", default="0,1,2,3")
+    ap.add_argument("--variants", default="")
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+    import leo_erasure_amd as le
+    torch.cuda.set_device(0)
+    assert le.gf_init() == "ok"
+    k, m, w = args.k, args.m, args.w
+    p = (k, m, w)
+    bs, _ = le.layout(args.coding, p, args.size)
+    n = args.objects
+    stride = max(k, m) * bs
+    objs = torch.zeros((n, stride), dtype=torch.uint8, device="cuda")
+    objs[:, :args.size].random_(0, 256)
+    par = torch.zeros((n, stride), dtype=torch.uint8, device="cuda")
+    ref = objs[:, :args.size].clone()
+    er = [int(x) for x in args.erased.split(",") if x]
+    e = len([x for x in er if x < k])
+    variants = [v.strip() for v in args.variants.split(";")]
+    keys = {kv.split("=")[0] for v in variants for kv in v.split(",") if kv}
+
+    def setenv(v):
+        for key in keys:
+            os.environ.pop(key, None)
+        for kv in v.split(","):
+            if kv:
+                a, b = kv.split("=")
+                os.environ[a] = b
+
+    ops = {"encode": (lambda: le.device.encode(args.coding, p, objs, args.size, par),
+                      (k + m) * bs * n)}
+    if er:
+        ops["decode%s" % er] = (lambda: le.device.decode(args.coding, p, objs, args.size, par, er),
+                                (k + e) * bs * n)
+    s = torch.cuda.current_stream()
+    res = {(v, o): [] for v in variants for o in ops}
+    ok = {}
+    for v in variants:  # correctness of every variant before timing
+        setenv(v)
+        ops["encode"][0]()
+        if er:
+            objs[:, :e * bs] = 0
+            list(ops.values())[1][0]()
+        torch.cuda.synchronize()
+        ok[v] = bool(torch.equal(objs[:, :args.size], ref))
+        objs[:, :args.size].copy_(ref)
+    for _ in range(args.rounds):
+        for v in variants:
+            setenv(v)
+            for o, (fn, _) in ops.items():
+                t0 = time.perf_counter()
+                while time.perf_counter() - t0 < 0.3:
+                    for _ in range(10):
+                        fn()
+                    torch.cuda.synchronize()
+                evs = []
+                for _ in range(args.reps):
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record(s)
+                    fn()
+                    b.record(s)
+                    evs.append((a, b))
+                torch.cuda.synchronize()
+                res[(v, o)].append(statistics.median(x.elapsed_time(y) for x, y in evs))
+    for (v, o), ts in res.items():
+        ms = statistics.median(ts)
+        alg = ops[o][1]
+        print(json.dumps({"config": f"{args.coding}{p}", "variant": v or "default", "op": o,
+                          "ms": round(ms, 4), "alg_GBps": round(alg / ms / 1e6, 1),
+                          "frac": round(alg / ms / 1e6 / 8000, 4), "correct": ok[v]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

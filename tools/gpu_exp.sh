@@ -13,6 +13,8 @@ for p in "${PARTS[@]}"; do
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     suite) step suite 900 python tools/bench_suite.py ${SUITE_ARGS:-} ;;
     e2e) step e2e 600 python tools/e2e_bench.py ;;
+    layout) step layout 600 python tools/layout_exp.py ${LAYOUT_ARGS:-} ;;
+    ab) step ab 900 python tools/env_ab.py ${AB_ARGS:-} ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     counters)
       cd /tmp && export TMPDIR=/tmp
