@@ -15,13 +15,14 @@ namespace {
 using GfbFn = int (*)(const GfBitApply&, int r0, int j0, int nk, uint64_t o0, uint64_t no,
                       hipStream_t);
 
-template <int W, int R, int LW, bool ACC>
+template <int W, int R, int LW, bool ACC, bool PF, bool CEIL = false, int KR = 0,
+          int WG = kThreads>
 int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
                  hipStream_t s) {
   GfbArgs<R> a;
   a.K = nk;
   a.ps = (uint32_t)(p.block_size / (uint64_t)W);
-  constexpr uint32_t tb = kThreads * 4u * LW;
+  constexpr uint32_t tb = WG * 4u * LW;
   a.tiles = (a.ps + tb - 1) / tb;
   for (int j = 0; j < kMaxK; ++j)
     a.in[j] = j < nk ? dev_shard(p.in[j0 + j], o0) : DevShard{nullptr, 0, 0, 0};
@@ -30,18 +31,21 @@ int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint6
     for (int j = 0; j < kMaxK; ++j)
       a.coef[i][j] = j < nk ? p.coef[(size_t)(r0 + i) * p.K + j0 + j] : 0u;
   }
-  hipLaunchKernelGGL((gfbit_apply<W, R, LW, ACC>), dim3((uint32_t)(no * a.tiles)),
-                     dim3(kThreads), 0, s, a);
+  if (KR > 0 && nk > KR) return LEOEC_E_ARG;
+  hipLaunchKernelGGL((gfbit_apply<W, R, LW, ACC, PF, CEIL, KR, WG>),
+                     dim3((uint32_t)(no * a.tiles)), dim3(WG), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }
 
-template <int W, int LW>
+constexpr bool kPF = true;  // one block of load look-ahead (kernels_impl.hpp gfbit_apply)
+
+template <int W, int LW, bool PF = kPF>
 GfbFn pick_r(int r, bool acc) {
   static const GfbFn tbl[2][kMaxR] = {
-      {&launch_gfb_t<W, 1, LW, false>, &launch_gfb_t<W, 2, LW, false>,
-       &launch_gfb_t<W, 3, LW, false>, &launch_gfb_t<W, 4, LW, false>},
-      {&launch_gfb_t<W, 1, LW, true>, &launch_gfb_t<W, 2, LW, true>,
-       &launch_gfb_t<W, 3, LW, true>, &launch_gfb_t<W, 4, LW, true>}};
+      {&launch_gfb_t<W, 1, LW, false, PF>, &launch_gfb_t<W, 2, LW, false, PF>,
+       &launch_gfb_t<W, 3, LW, false, PF>, &launch_gfb_t<W, 4, LW, false, PF>},
+      {&launch_gfb_t<W, 1, LW, true, PF>, &launch_gfb_t<W, 2, LW, true, PF>,
+       &launch_gfb_t<W, 3, LW, true, PF>, &launch_gfb_t<W, 4, LW, true, PF>}};
   return tbl[acc ? 1 : 0][r - 1];
 }
 
@@ -52,9 +56,36 @@ int lane_width_env() {
   return e ? std::atoi(e) : 2;
 }
 
-GfbFn pick(int w, int r, bool acc) {
+// LEOEC_GFBIT_PF=0|1 toggles the load look-ahead for w = 8 measurements.
+bool prefetch_env() {
+  const char* e = std::getenv("LEOEC_GFBIT_PF");
+  return e ? std::atoi(e) != 0 : kPF;
+}
+
+GfbFn pick(int w, int r, bool acc, int nk) {
   if (w == 8) {
     const int lw = lane_width_env();
+    const char* ce = std::getenv("LEOEC_GFBIT_CEIL");  // measurement only: not a code
+    if (ce && std::atoi(ce) && r == 4 && !acc) return &launch_gfb_t<8, 4, 2, false, kPF, true>;
+    // LEOEC_GFBIT_WG=128|512|1024 (measurement): workgroup size, LW 2 / PF
+    if (const char* wg = std::getenv("LEOEC_GFBIT_WG")) {
+      if (r == 4 && !acc && std::atoi(wg) == 128) return &launch_gfb_t<8, 4, 2, false, kPF, false, 0, 128>;
+      if (r == 4 && !acc && std::atoi(wg) == 512) return &launch_gfb_t<8, 4, 2, false, kPF, false, 0, 512>;
+      if (r == 4 && !acc && std::atoi(wg) == 1024) return &launch_gfb_t<8, 4, 2, false, kPF, false, 0, 1024>;
+      if (r == 4 && !acc && std::atoi(wg) == 5121) return &launch_gfb_t<8, 4, 1, false, kPF, false, 0, 512>;
+      if (r == 4 && !acc && std::atoi(wg) == 10241) return &launch_gfb_t<8, 4, 1, false, kPF, false, 0, 1024>;
+    }
+    // LEOEC_GFBIT_RES=1|2 (measurement): all <= 10 input blocks resident, LW 1|2
+    const char* re = std::getenv("LEOEC_GFBIT_RES");
+    if (re && r == 4 && !acc && nk <= 10) {
+      if (std::atoi(re) == 1) return &launch_gfb_t<8, 4, 1, false, kPF, false, 10>;
+      if (std::atoi(re) == 2) return &launch_gfb_t<8, 4, 2, false, kPF, false, 10>;
+    }
+    if (prefetch_env() != kPF) {
+      if (lw == 1) return pick_r<8, 1, !kPF>(r, acc);
+      if (lw == 4) return pick_r<8, 4, !kPF>(r, acc);
+      return pick_r<8, 2, !kPF>(r, acc);
+    }
     if (lw == 1) return pick_r<8, 1>(r, acc);
     if (lw == 4) return pick_r<8, 4>(r, acc);
     return pick_r<8, 2>(r, acc);
@@ -102,7 +133,7 @@ int launch(const GfBitApply& p, hipStream_t s) {
       const int nr = (p.R - r0 < kMaxR) ? p.R - r0 : kMaxR;
       for (int j0 = 0; j0 < p.K; j0 += kMaxK) {
         const int nk = (p.K - j0 < kMaxK) ? p.K - j0 : kMaxK;
-        const int rc = pick(w, nr, j0 > 0)(p, r0, j0, nk, o0, no, s);
+        const int rc = pick(w, nr, j0 > 0, nk)(p, r0, j0, nk, o0, no, s);
         if (rc) return rc;
       }
     }

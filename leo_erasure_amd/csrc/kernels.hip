@@ -51,6 +51,35 @@ ChunkFn gfw_pick(int r, bool acc) {
 
 // LEOEC_GF8_VARIANT=<n> selects a measurement variant of gf8_apply<10,4>
 // (tools/kvariants.py); unset or 0 = the shipped kernel.
+// LEOEC_BIT_FORM selects the bitmatrix kernel form for measurements:
+// 0 masked (no look-ahead), 1 masked + look-ahead (shipped), 2 branchy,
+// 3 branchy + look-ahead.  Measured on liberation(7,2,7): 1 is best — the
+// scalar branches of 2/3 cost more than the masked xors they save.
+int bit_form_env() {
+  const char* e = std::getenv("LEOEC_BIT_FORM");
+  const int f = e ? std::atoi(e) : 1;
+  return (f >= 0 && f <= 3) ? f : 1;
+}
+
+using BitFn = void (*)(const detail::BitArgs);
+
+template <int RO, bool ACC>
+BitFn bit_kernel_f(int form) {
+  switch (form) {
+    case 0: return &detail::bit_apply<RO, ACC, false, false>;
+    case 1: return &detail::bit_apply<RO, ACC, false, true>;
+    case 2: return &detail::bit_apply<RO, ACC, true, false>;
+    case 3: return &detail::bit_apply<RO, ACC, true, true>;
+    default: return &detail::bit_apply<RO, ACC, false, true>;
+  }
+}
+
+BitFn bit_kernel(int ro, bool acc, int form) {
+  if (ro == 8) return acc ? bit_kernel_f<8, true>(form) : bit_kernel_f<8, false>(form);
+  if (ro == 16) return acc ? bit_kernel_f<16, true>(form) : bit_kernel_f<16, false>(form);
+  return acc ? bit_kernel_f<32, true>(form) : bit_kernel_f<32, false>(form);
+}
+
 int gf8_variant_env() {
   const char* e = std::getenv("LEOEC_GF8_VARIANT");
   return e ? std::atoi(e) : 0;
@@ -156,16 +185,9 @@ int launch(const BitApply& p, hipStream_t s) {
         }
         const bool acc = j0 > 0;
         const dim3 grid((uint32_t)(no * tiles)), block(kThreads);
-        if (RP <= 8) {
-          if (acc) hipLaunchKernelGGL((bit_apply<8, true>), grid, block, 0, s, a);
-          else hipLaunchKernelGGL((bit_apply<8, false>), grid, block, 0, s, a);
-        } else if (RP <= 16) {
-          if (acc) hipLaunchKernelGGL((bit_apply<16, true>), grid, block, 0, s, a);
-          else hipLaunchKernelGGL((bit_apply<16, false>), grid, block, 0, s, a);
-        } else {
-          if (acc) hipLaunchKernelGGL((bit_apply<32, true>), grid, block, 0, s, a);
-          else hipLaunchKernelGGL((bit_apply<32, false>), grid, block, 0, s, a);
-        }
+        const int form = bit_form_env();
+        const int ro = RP <= 8 ? 8 : RP <= 16 ? 16 : 32;
+        hipLaunchKernelGGL(bit_kernel(ro, acc, form), grid, block, 0, s, a);
         if (hipGetLastError() != hipSuccess) return LEOEC_E_HIP;
       }
     }

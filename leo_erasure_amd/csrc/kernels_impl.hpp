@@ -513,7 +513,12 @@ struct BitArgs {
   uint32_t tiles;              // tiles per object (over one packet)
 };
 
-template <int RO, bool ACC>
+// BR: per (input packet, output packet) pair a wave-uniform branch on the
+// bitmatrix bit (scalar unit) and a plain xor when set, instead of a masked
+// xor for every pair (vector unit) — the bitmatrices of liberation and of
+// decode maps are sparse.  PF: the next input packet's load is issued before
+// the current one is applied.
+template <int RO, bool ACC, bool BR = false, bool PF = true>
 __global__ void __launch_bounds__(kThreads) bit_apply(const BitArgs a) {
   const uint32_t obj = blockIdx.x / a.tiles;
   const uint32_t tile = blockIdx.x - obj * a.tiles;
@@ -526,23 +531,42 @@ __global__ void __launch_bounds__(kThreads) bit_apply(const BitArgs a) {
     acc[o] = u32x4{0u, 0u, 0u, 0u};
     if (ACC) acc[o] = load_guarded(a.out[o].base + o64 * a.out[o].stride, off, a.out[o].valid);
   }
-  int blk = 0, x = 0;
-  for (int p = 0; p < a.KP; ++p) {
+  auto load_packet = [&](int blk, int x) {
     const uint32_t pk = (uint32_t)x * a.ps;
     const uint32_t bv = a.in[blk].valid;
-    const uint32_t valid = bv > pk ? bv - pk : 0u;
-    const u32x4 v = load_guarded(a.in[blk].base + o64 * a.in[blk].stride + pk, off, valid);
+    return load_guarded(a.in[blk].base + o64 * a.in[blk].stride + pk, off, bv > pk ? bv - pk : 0u);
+  };
+  int blk = 0, x = 0;
+  u32x4 v = PF ? load_packet(0, 0) : u32x4{0u, 0u, 0u, 0u};
+  for (int p = 0; p < a.KP; ++p) {
+    int nblk = blk, nx = x + 1;
+    if (nx == a.w) {
+      nx = 0;
+      ++nblk;
+    }
+    u32x4 vn = v;
+    if (PF) {
+      if (p + 1 < a.KP) vn = load_packet(nblk, nx);
+    } else {
+      v = load_packet(blk, x);
+    }
     const uint32_t bits = a.bits[p];
 #pragma unroll
     for (int o = 0; o < RO; ++o) {
-      const uint32_t m = (uint32_t)((int32_t)(bits << o) >> 31);
+      if (BR) {
+        if ((bits << o) & 0x80000000u) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[o][e] ^= v[e] & m;
+          for (int e = 0; e < 4; ++e) acc[o][e] ^= v[e];
+        }
+      } else {
+        const uint32_t m = (uint32_t)((int32_t)(bits << o) >> 31);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[o][e] ^= v[e] & m;
+      }
     }
-    if (++x == a.w) {
-      x = 0;
-      ++blk;
-    }
+    if (PF) v = vn;
+    blk = nblk;
+    x = nx;
   }
 #pragma unroll
   for (int o = 0; o < RO; ++o) {
@@ -647,12 +671,68 @@ __device__ __forceinline__ void lv_store(uint8_t* p, uint32_t off, uint32_t vali
   }
 }
 
-template <int W, int R, int LW, bool ACC>
-__global__ void __launch_bounds__(kThreads) gfbit_apply(const GfbArgs<R> a) {
+template <int W, int LW>
+__device__ __forceinline__ void gfb_load_block(const uint8_t* base, uint32_t ps, uint32_t off,
+                                               uint32_t bv, LaneVec<LW> (&y)[W]) {
+#pragma unroll
+  for (int x = 0; x < W; ++x) {
+    const uint32_t pk = (uint32_t)x * ps;
+    y[x] = lv_load<LW>(base + pk, off, bv > pk ? bv - pk : 0u);
+  }
+}
+
+// acc[i] ^= c[i] * y for every output i (y is consumed: it is doubled in
+// place).  CEIL (measurement only): every input xor-ed into every output, no
+// GF arithmetic — the memory ceiling of the access pattern, not a code.
+template <int W, int R, int LW, bool CEIL>
+__device__ __forceinline__ void gfb_accumulate(LaneVec<LW> (&acc)[R][W], LaneVec<LW> (&y)[W],
+                                               const uint32_t (&c)[R]) {
+  if (CEIL) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int x = 0; x < W; ++x)
+#pragma unroll
+        for (int e = 0; e < LW; ++e) acc[i][x].v[e] ^= y[x].v[e];
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < W; ++t) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if ((c[i] >> t) & 1u) {
+#pragma unroll
+        for (int x = 0; x < W; ++x)
+#pragma unroll
+          for (int e = 0; e < LW; ++e) acc[i][x].v[e] ^= y[x].v[e];
+      }
+    }
+    if (t + 1 < W) {  // y <- y * 2
+      const LaneVec<LW> top = y[W - 1];
+#pragma unroll
+      for (int r = W - 1; r >= 1; --r) {
+#pragma unroll
+        for (int e = 0; e < LW; ++e)
+          y[r].v[e] = ((DefaultPoly<W>::v >> r) & 1u) ? (y[r - 1].v[e] ^ top.v[e]) : y[r - 1].v[e];
+      }
+      y[0] = top;
+    }
+  }
+}
+
+// Input staging forms:
+//   KR > 0 : all (<= KR) input blocks are loaded before any arithmetic, so a
+//            wave has every load of its tile in flight at once (like gf8);
+//   PF     : one block of look-ahead — block j+1's loads are issued before
+//            the arithmetic on block j;
+//   neither: load block j, then compute on it.
+template <int W, int R, int LW, bool ACC, bool PF = true, bool CEIL = false, int KR = 0,
+          int WG = kThreads>
+__global__ void __launch_bounds__(WG) gfbit_apply(const GfbArgs<R> a) {
   constexpr uint32_t LB = 4u * LW;
   const uint32_t obj = blockIdx.x / a.tiles;
   const uint32_t tile = blockIdx.x - obj * a.tiles;
-  const uint32_t off = tile * (kThreads * LB) + threadIdx.x * LB;
+  const uint32_t off = tile * (WG * LB) + threadIdx.x * LB;
   if (off >= a.ps) return;
   const uint64_t o64 = obj;
   LaneVec<LW> acc[R][W];
@@ -670,38 +750,43 @@ __global__ void __launch_bounds__(kThreads) gfbit_apply(const GfbArgs<R> a) {
         for (int e = 0; e < LW; ++e) acc[i][x].v[e] = 0u;
       }
     }
-  for (int j = 0; j < a.K; ++j) {
-    const uint8_t* base = a.in[j].base + o64 * a.in[j].stride;
-    const uint32_t bv = a.in[j].valid;
-    LaneVec<LW> y[W];
-#pragma unroll
-    for (int x = 0; x < W; ++x) {
-      const uint32_t pk = (uint32_t)x * a.ps;
-      y[x] = lv_load<LW>(base + pk, off, bv > pk ? bv - pk : 0u);
-    }
-    uint32_t c[R];
+  auto coefs = [&](int j, uint32_t (&c)[R]) {
 #pragma unroll
     for (int i = 0; i < R; ++i) c[i] = a.coef[i][j];
+  };
+  if constexpr (KR > 0) {
+    LaneVec<LW> ys[KR][W];
 #pragma unroll
-    for (int t = 0; t < W; ++t) {
+    for (int j = 0; j < KR; ++j)
+      if (j < a.K)
+        gfb_load_block<W, LW>(a.in[j].base + o64 * a.in[j].stride, a.ps, off, a.in[j].valid,
+                              ys[j]);
 #pragma unroll
-      for (int i = 0; i < R; ++i) {
-        if ((c[i] >> t) & 1u) {
-#pragma unroll
-          for (int x = 0; x < W; ++x)
-#pragma unroll
-            for (int e = 0; e < LW; ++e) acc[i][x].v[e] ^= y[x].v[e];
-        }
+    for (int j = 0; j < KR; ++j) {
+      if (j < a.K) {
+        uint32_t c[R];
+        coefs(j, c);
+        gfb_accumulate<W, R, LW, CEIL>(acc, ys[j], c);
       }
-      if (t + 1 < W) {  // y <- y * 2
-        const LaneVec<LW> top = y[W - 1];
+    }
+  } else {
+    LaneVec<LW> y[W], yn[W];
+    if (PF)
+      gfb_load_block<W, LW>(a.in[0].base + o64 * a.in[0].stride, a.ps, off, a.in[0].valid, y);
+    for (int j = 0; j < a.K; ++j) {
+      if (PF) {
+        if (j + 1 < a.K)
+          gfb_load_block<W, LW>(a.in[j + 1].base + o64 * a.in[j + 1].stride, a.ps, off,
+                                a.in[j + 1].valid, yn);
+      } else {
+        gfb_load_block<W, LW>(a.in[j].base + o64 * a.in[j].stride, a.ps, off, a.in[j].valid, y);
+      }
+      uint32_t c[R];
+      coefs(j, c);
+      gfb_accumulate<W, R, LW, CEIL>(acc, y, c);
+      if (PF) {
 #pragma unroll
-        for (int r = W - 1; r >= 1; --r) {
-#pragma unroll
-          for (int e = 0; e < LW; ++e)
-            y[r].v[e] = ((DefaultPoly<W>::v >> r) & 1u) ? (y[r - 1].v[e] ^ top.v[e]) : y[r - 1].v[e];
-        }
-        y[0] = top;
+        for (int x = 0; x < W; ++x) y[x] = yn[x];
       }
     }
   }

@@ -258,7 +258,12 @@ def test_device_roundtrip_bench_shape(gpu, le):
 
 
 @pytest.mark.parametrize("env", [{"LEOEC_BITMATRIX": "1"}, {"LEOEC_GFBIT_LW": "1"},
-                                 {"LEOEC_GFBIT_LW": "4"}], ids=lambda e: ",".join(e))
+                                 {"LEOEC_GFBIT_LW": "4"}, {"LEOEC_GFBIT_PF": "0"},
+                                 {"LEOEC_GFBIT_PF": "0", "LEOEC_GFBIT_LW": "1"},
+                                 {"LEOEC_BITMATRIX": "1", "LEOEC_BIT_FORM": "0"},
+                                 {"LEOEC_BITMATRIX": "1", "LEOEC_BIT_FORM": "1"},
+                                 {"LEOEC_BITMATRIX": "1", "LEOEC_BIT_FORM": "2"}],
+                         ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_cauchy_kernel_forms_agree(gpu, le, oracle, env, monkeypatch):
     """cauchyrs through the generic masked-bitmatrix kernel and through every
     lane width of the bitsliced GF kernel gives the oracle's bytes."""
@@ -271,6 +276,23 @@ def test_cauchy_kernel_forms_agree(gpu, le, oracle, env, monkeypatch):
         ids = list(range(m, k + m))
         st, out = le.nif_decode(cls, (k, m, w), [blocks[i] for i in ids], ids, len(data))
         assert st == "ok" and out == data
+
+
+@pytest.mark.parametrize("form", ["0", "1", "2", "3"])
+def test_bitmatrix_kernel_forms_agree(gpu, le, oracle, form, monkeypatch):
+    """liberation (and >32 output packets: w = 17 cauchy) through every form of
+    the bitmatrix kernel: masked / branchy, with and without look-ahead."""
+    monkeypatch.setenv("LEOEC_BIT_FORM", form)
+    for cls, k, m, w in [("liberation", 7, 2, 7), ("liberation", 3, 2, 31),
+                         ("cauchyrs", 5, 3, 17)]:
+        data = rand_bytes(150001, k + w)
+        st, blocks = le.nif_encode(cls, (k, m, w), data, len(data))
+        assert st == "ok" and blocks == oracle.encode(cls, k, m, w, data)
+        ids = list(range(m, k + m))
+        st, out = le.nif_decode(cls, (k, m, w), [blocks[i] for i in ids], ids, len(data))
+        assert st == "ok" and out == data
+        st, rep = le.nif_repair(cls, (k, m, w), [blocks[i] for i in ids], ids, [0, k])
+        assert st == "ok" and rep == [blocks[0], blocks[k]]
 
 
 def test_golden_fixtures_gpu(gpu, le):
