@@ -15,8 +15,8 @@ namespace {
 using GfbFn = int (*)(const GfBitApply&, int r0, int j0, int nk, uint64_t o0, uint64_t no,
                       hipStream_t);
 
-template <int W, int R, int LW, bool ACC, bool PF, bool CEIL = false, int KR = 0,
-          int WG = kThreads>
+template <int W, int R, int LW, bool ACC, int PF, bool CEIL = false, int KR = 0,
+          int WG = kThreads, bool XMAP = false>
 int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
                  hipStream_t s) {
   GfbArgs<R> a;
@@ -32,14 +32,33 @@ int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint6
       a.coef[i][j] = j < nk ? p.coef[(size_t)(r0 + i) * p.K + j0 + j] : 0u;
   }
   if (KR > 0 && nk > KR) return LEOEC_E_ARG;
-  hipLaunchKernelGGL((gfbit_apply<W, R, LW, ACC, PF, CEIL, KR, WG>),
+  hipLaunchKernelGGL((gfbit_apply<W, R, LW, ACC, PF, CEIL, KR, WG, XMAP>),
                      dim3((uint32_t)(no * a.tiles)), dim3(WG), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }
 
-constexpr bool kPF = true;  // one block of load look-ahead (kernels_impl.hpp gfbit_apply)
+constexpr int kPF = 1;  // blocks of load look-ahead (kernels_impl.hpp gfbit_apply)
 
-template <int W, int LW, bool PF = kPF>
+template <int W, int R, bool ACC>
+int launch_gfb_lds_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
+                     hipStream_t s) {
+  GfbArgs<R> a;
+  a.K = nk;
+  a.ps = (uint32_t)(p.block_size / (uint64_t)W);
+  a.tiles = (a.ps + kGfbLdsSlice - 1) / kGfbLdsSlice;
+  for (int j = 0; j < kMaxK; ++j)
+    a.in[j] = j < nk ? dev_shard(p.in[j0 + j], o0) : DevShard{nullptr, 0, 0, 0};
+  for (int i = 0; i < R; ++i) {
+    a.out[i] = dev_shard(p.out[r0 + i], o0);
+    for (int j = 0; j < kMaxK; ++j)
+      a.coef[i][j] = j < nk ? p.coef[(size_t)(r0 + i) * p.K + j0 + j] : 0u;
+  }
+  hipLaunchKernelGGL((gfbit_lds_apply<W, R, ACC>), dim3((uint32_t)(no * a.tiles)),
+                     dim3(kGfbLdsThreads), 0, s, a);
+  return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
+}
+
+template <int W, int LW, int PF = kPF>
 GfbFn pick_r(int r, bool acc) {
   static const GfbFn tbl[2][kMaxR] = {
       {&launch_gfb_t<W, 1, LW, false, PF>, &launch_gfb_t<W, 2, LW, false, PF>,
@@ -56,10 +75,11 @@ int lane_width_env() {
   return e ? std::atoi(e) : 2;
 }
 
-// LEOEC_GFBIT_PF=0|1 toggles the load look-ahead for w = 8 measurements.
-bool prefetch_env() {
+// LEOEC_GFBIT_PF=0|1|2|3 sets the load look-ahead (blocks) for w = 8
+// measurements.
+int prefetch_env() {
   const char* e = std::getenv("LEOEC_GFBIT_PF");
-  return e ? std::atoi(e) != 0 : kPF;
+  return e ? std::atoi(e) : kPF;
 }
 
 GfbFn pick(int w, int r, bool acc, int nk) {
@@ -67,24 +87,33 @@ GfbFn pick(int w, int r, bool acc, int nk) {
     const int lw = lane_width_env();
     const char* ce = std::getenv("LEOEC_GFBIT_CEIL");  // measurement only: not a code
     if (ce && std::atoi(ce) && r == 4 && !acc) return &launch_gfb_t<8, 4, 2, false, kPF, true>;
-    // LEOEC_GFBIT_WG=128|512|1024 (measurement): workgroup size, LW 2 / PF
-    if (const char* wg = std::getenv("LEOEC_GFBIT_WG")) {
-      if (r == 4 && !acc && std::atoi(wg) == 128) return &launch_gfb_t<8, 4, 2, false, kPF, false, 0, 128>;
-      if (r == 4 && !acc && std::atoi(wg) == 512) return &launch_gfb_t<8, 4, 2, false, kPF, false, 0, 512>;
-      if (r == 4 && !acc && std::atoi(wg) == 1024) return &launch_gfb_t<8, 4, 2, false, kPF, false, 0, 1024>;
-      if (r == 4 && !acc && std::atoi(wg) == 5121) return &launch_gfb_t<8, 4, 1, false, kPF, false, 0, 512>;
-      if (r == 4 && !acc && std::atoi(wg) == 10241) return &launch_gfb_t<8, 4, 1, false, kPF, false, 0, 1024>;
+    // LEOEC_GFBIT_XMAP=1 (measurement): all tiles of an object on one XCD
+    if (const char* xm = std::getenv("LEOEC_GFBIT_XMAP"))
+      if (std::atoi(xm) && r == 4 && !acc) return &launch_gfb_t<8, 4, 2, false, kPF, false, 0, kThreads, true>;
+    // LEOEC_GFBIT_LDS=1 (measurement): LDS-staged inputs
+    if (const char* le = std::getenv("LEOEC_GFBIT_LDS")) {
+      if (std::atoi(le) == 1) {
+        static const GfbFn tbl[2][kMaxR] = {
+            {&launch_gfb_lds_t<8, 1, false>, &launch_gfb_lds_t<8, 2, false>,
+             &launch_gfb_lds_t<8, 3, false>, &launch_gfb_lds_t<8, 4, false>},
+            {&launch_gfb_lds_t<8, 1, true>, &launch_gfb_lds_t<8, 2, true>,
+             &launch_gfb_lds_t<8, 3, true>, &launch_gfb_lds_t<8, 4, true>}};
+        return tbl[acc ? 1 : 0][r - 1];
+      }
     }
-    // LEOEC_GFBIT_RES=1|2 (measurement): all <= 10 input blocks resident, LW 1|2
-    const char* re = std::getenv("LEOEC_GFBIT_RES");
-    if (re && r == 4 && !acc && nk <= 10) {
-      if (std::atoi(re) == 1) return &launch_gfb_t<8, 4, 1, false, kPF, false, 10>;
-      if (std::atoi(re) == 2) return &launch_gfb_t<8, 4, 2, false, kPF, false, 10>;
+    const int pf = prefetch_env();
+    if (pf == 0) {
+      if (lw == 1) return pick_r<8, 1, 0>(r, acc);
+      if (lw == 4) return pick_r<8, 4, 0>(r, acc);
+      return pick_r<8, 2, 0>(r, acc);
     }
-    if (prefetch_env() != kPF) {
-      if (lw == 1) return pick_r<8, 1, !kPF>(r, acc);
-      if (lw == 4) return pick_r<8, 4, !kPF>(r, acc);
-      return pick_r<8, 2, !kPF>(r, acc);
+    if (pf == 2) {
+      if (lw == 1) return pick_r<8, 1, 2>(r, acc);
+      return pick_r<8, 2, 2>(r, acc);
+    }
+    if (pf == 3) {
+      if (lw == 1) return pick_r<8, 1, 3>(r, acc);
+      return pick_r<8, 2, 3>(r, acc);
     }
     if (lw == 1) return pick_r<8, 1>(r, acc);
     if (lw == 4) return pick_r<8, 4>(r, acc);

@@ -52,13 +52,16 @@ ChunkFn gfw_pick(int r, bool acc) {
 // LEOEC_GF8_VARIANT=<n> selects a measurement variant of gf8_apply<10,4>
 // (tools/kvariants.py); unset or 0 = the shipped kernel.
 // LEOEC_BIT_FORM selects the bitmatrix kernel form for measurements:
-// 0 masked (no look-ahead), 1 masked + look-ahead (shipped), 2 branchy,
-// 3 branchy + look-ahead.  Measured on liberation(7,2,7): 1 is best — the
-// scalar branches of 2/3 cost more than the masked xors they save.
+//   0 masked, no look-ahead        1 masked, 1 packet ahead
+//   2 branchy, no look-ahead       3 branchy, 1 packet ahead
+//   4/5/6 masked, 2/3/5 packets ahead (4 = shipped)
+//   7 as 4, with all tiles of an object on one XCD
+// Measured on liberation(7,2,7): masked beats branchy (the scalar branches
+// cost more than the masked xors they save); look-ahead depth see DESIGN.md.
 int bit_form_env() {
   const char* e = std::getenv("LEOEC_BIT_FORM");
-  const int f = e ? std::atoi(e) : 1;
-  return (f >= 0 && f <= 3) ? f : 1;
+  const int f = e ? std::atoi(e) : 4;
+  return (f >= 0 && f <= 7) ? f : 4;
 }
 
 using BitFn = void (*)(const detail::BitArgs);
@@ -66,11 +69,14 @@ using BitFn = void (*)(const detail::BitArgs);
 template <int RO, bool ACC>
 BitFn bit_kernel_f(int form) {
   switch (form) {
-    case 0: return &detail::bit_apply<RO, ACC, false, false>;
-    case 1: return &detail::bit_apply<RO, ACC, false, true>;
-    case 2: return &detail::bit_apply<RO, ACC, true, false>;
-    case 3: return &detail::bit_apply<RO, ACC, true, true>;
-    default: return &detail::bit_apply<RO, ACC, false, true>;
+    case 0: return &detail::bit_apply<RO, ACC, false, 0>;
+    case 1: return &detail::bit_apply<RO, ACC, false, 1>;
+    case 2: return &detail::bit_apply<RO, ACC, true, 0>;
+    case 3: return &detail::bit_apply<RO, ACC, true, 1>;
+    case 5: return &detail::bit_apply<RO, ACC, false, 3>;
+    case 6: return &detail::bit_apply<RO, ACC, false, 5>;
+    case 7: return &detail::bit_apply<RO, ACC, false, 2, true>;
+    default: return &detail::bit_apply<RO, ACC, false, 2>;
   }
 }
 

@@ -515,13 +515,16 @@ struct BitArgs {
 
 // BR: per (input packet, output packet) pair a wave-uniform branch on the
 // bitmatrix bit (scalar unit) and a plain xor when set, instead of a masked
-// xor for every pair (vector unit) — the bitmatrices of liberation and of
-// decode maps are sparse.  PF: the next input packet's load is issued before
-// the current one is applied.
-template <int RO, bool ACC, bool BR = false, bool PF = true>
+// xor for every pair (vector unit).  PFD: loads of the next PFD input packets
+// are kept in flight while one is applied (a ring of PFD+1 registers).  A
+// streaming kernel needs ~50 KB in flight per CU to cover HBM latency; with
+// one packet at a time a wave holds only 1 KiB.
+template <int RO, bool ACC, bool BR = false, int PFD = 1, bool XMAP = false>
 __global__ void __launch_bounds__(kThreads) bit_apply(const BitArgs a) {
-  const uint32_t obj = blockIdx.x / a.tiles;
-  const uint32_t tile = blockIdx.x - obj * a.tiles;
+  constexpr int RS = PFD + 1;
+  const uint32_t bid = XMAP ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t obj = bid / a.tiles;
+  const uint32_t tile = bid - obj * a.tiles;
   const uint32_t off = tile * kTileBytes + threadIdx.x * 16u;
   if (off >= a.ps) return;
   const uint64_t o64 = obj;
@@ -531,42 +534,38 @@ __global__ void __launch_bounds__(kThreads) bit_apply(const BitArgs a) {
     acc[o] = u32x4{0u, 0u, 0u, 0u};
     if (ACC) acc[o] = load_guarded(a.out[o].base + o64 * a.out[o].stride, off, a.out[o].valid);
   }
-  auto load_packet = [&](int blk, int x) {
+  auto load_packet = [&](int p) {
+    const int blk = p / a.w, x = p - blk * a.w;  // wave-uniform
     const uint32_t pk = (uint32_t)x * a.ps;
     const uint32_t bv = a.in[blk].valid;
     return load_guarded(a.in[blk].base + o64 * a.in[blk].stride + pk, off, bv > pk ? bv - pk : 0u);
   };
-  int blk = 0, x = 0;
-  u32x4 v = PF ? load_packet(0, 0) : u32x4{0u, 0u, 0u, 0u};
-  for (int p = 0; p < a.KP; ++p) {
-    int nblk = blk, nx = x + 1;
-    if (nx == a.w) {
-      nx = 0;
-      ++nblk;
-    }
-    u32x4 vn = v;
-    if (PF) {
-      if (p + 1 < a.KP) vn = load_packet(nblk, nx);
-    } else {
-      v = load_packet(blk, x);
-    }
-    const uint32_t bits = a.bits[p];
+  u32x4 ring[RS];
 #pragma unroll
-    for (int o = 0; o < RO; ++o) {
-      if (BR) {
-        if ((bits << o) & 0x80000000u) {
+  for (int u = 0; u < PFD; ++u) ring[u] = u < a.KP ? load_packet(u) : u32x4{0u, 0u, 0u, 0u};
+  for (int p0 = 0; p0 < a.KP; p0 += RS) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[o][e] ^= v[e];
+    for (int u = 0; u < RS; ++u) {
+      const int p = p0 + u;
+      if (p < a.KP) {
+        if (p + PFD < a.KP) ring[(u + PFD) % RS] = load_packet(p + PFD);
+        const u32x4 v = ring[u];
+        const uint32_t bits = a.bits[p];
+#pragma unroll
+        for (int o = 0; o < RO; ++o) {
+          if (BR) {
+            if ((bits << o) & 0x80000000u) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc[o][e] ^= v[e];
+            }
+          } else {
+            const uint32_t m = (uint32_t)((int32_t)(bits << o) >> 31);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[o][e] ^= v[e] & m;
+          }
         }
-      } else {
-        const uint32_t m = (uint32_t)((int32_t)(bits << o) >> 31);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[o][e] ^= v[e] & m;
       }
     }
-    if (PF) v = vn;
-    blk = nblk;
-    x = nx;
   }
 #pragma unroll
   for (int o = 0; o < RO; ++o) {
@@ -723,15 +722,16 @@ __device__ __forceinline__ void gfb_accumulate(LaneVec<LW> (&acc)[R][W], LaneVec
 // Input staging forms:
 //   KR > 0 : all (<= KR) input blocks are loaded before any arithmetic, so a
 //            wave has every load of its tile in flight at once (like gf8);
-//   PF     : one block of look-ahead — block j+1's loads are issued before
-//            the arithmetic on block j;
-//   neither: load block j, then compute on it.
-template <int W, int R, int LW, bool ACC, bool PF = true, bool CEIL = false, int KR = 0,
-          int WG = kThreads>
+//   PFD > 0: the loads of the next PFD blocks are in flight while block j is
+//            computed (a ring of PFD+1 blocks in VGPRs);
+//   PFD = 0: load block j, then compute on it.
+template <int W, int R, int LW, bool ACC, int PFD = 1, bool CEIL = false, int KR = 0,
+          int WG = kThreads, bool XMAP = false>
 __global__ void __launch_bounds__(WG) gfbit_apply(const GfbArgs<R> a) {
   constexpr uint32_t LB = 4u * LW;
-  const uint32_t obj = blockIdx.x / a.tiles;
-  const uint32_t tile = blockIdx.x - obj * a.tiles;
+  const uint32_t bid = XMAP ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t obj = bid / a.tiles;
+  const uint32_t tile = bid - obj * a.tiles;
   const uint32_t off = tile * (WG * LB) + threadIdx.x * LB;
   if (off >= a.ps) return;
   const uint64_t o64 = obj;
@@ -754,13 +754,14 @@ __global__ void __launch_bounds__(WG) gfbit_apply(const GfbArgs<R> a) {
 #pragma unroll
     for (int i = 0; i < R; ++i) c[i] = a.coef[i][j];
   };
+  auto load = [&](int j, LaneVec<LW> (&y)[W]) {
+    gfb_load_block<W, LW>(a.in[j].base + o64 * a.in[j].stride, a.ps, off, a.in[j].valid, y);
+  };
   if constexpr (KR > 0) {
     LaneVec<LW> ys[KR][W];
 #pragma unroll
     for (int j = 0; j < KR; ++j)
-      if (j < a.K)
-        gfb_load_block<W, LW>(a.in[j].base + o64 * a.in[j].stride, a.ps, off, a.in[j].valid,
-                              ys[j]);
+      if (j < a.K) load(j, ys[j]);
 #pragma unroll
     for (int j = 0; j < KR; ++j) {
       if (j < a.K) {
@@ -770,26 +771,122 @@ __global__ void __launch_bounds__(WG) gfbit_apply(const GfbArgs<R> a) {
       }
     }
   } else {
-    LaneVec<LW> y[W], yn[W];
-    if (PF)
-      gfb_load_block<W, LW>(a.in[0].base + o64 * a.in[0].stride, a.ps, off, a.in[0].valid, y);
-    for (int j = 0; j < a.K; ++j) {
-      if (PF) {
-        if (j + 1 < a.K)
-          gfb_load_block<W, LW>(a.in[j + 1].base + o64 * a.in[j + 1].stride, a.ps, off,
-                                a.in[j + 1].valid, yn);
-      } else {
-        gfb_load_block<W, LW>(a.in[j].base + o64 * a.in[j].stride, a.ps, off, a.in[j].valid, y);
-      }
-      uint32_t c[R];
-      coefs(j, c);
-      gfb_accumulate<W, R, LW, CEIL>(acc, y, c);
-      if (PF) {
+    constexpr int RS = PFD + 1;
+    LaneVec<LW> ring[RS][W];
 #pragma unroll
-        for (int x = 0; x < W; ++x) y[x] = yn[x];
+    for (int u = 0; u < PFD; ++u)
+      if (u < a.K) load(u, ring[u]);
+    for (int j0 = 0; j0 < a.K; j0 += RS) {
+#pragma unroll
+      for (int u = 0; u < RS; ++u) {
+        const int j = j0 + u;
+        if (j < a.K) {
+          if (j + PFD < a.K) load(j + PFD, ring[(u + PFD) % RS]);
+          uint32_t c[R];
+          coefs(j, c);
+          gfb_accumulate<W, R, LW, CEIL>(acc, ring[u], c);
+        }
       }
     }
   }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    uint8_t* p = const_cast<uint8_t*>(a.out[i].base) + o64 * a.out[i].stride;
+    const uint32_t bv = a.out[i].valid;
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const uint32_t pk = (uint32_t)x * a.ps;
+      lv_store<LW>(p + pk, off, bv > pk ? bv - pk : 0u, acc[i][x]);
+    }
+  }
+}
+
+// LDS-staged form of gfbit_apply.  The workgroup stages each input block's
+// W packet slices (2 KiB each) through LDS: wave v loads half-packets, so a
+// wave streams ceil(W/2) packets of 1 KiB contiguous per block instead of W
+// packets of 512 B, and block j+1's loads are in flight (in VGPRs) while
+// block j is computed from LDS.  Lanes then read their 8-byte columns of all
+// W packets from LDS (conflict-free ds_read_b64) and run the same bitsliced
+// arithmetic.  Outputs are stored directly.
+constexpr int kGfbLdsThreads = 256;
+constexpr uint32_t kGfbLdsSlice = kGfbLdsThreads * 8u;  // bytes per packet per tile
+
+template <int W, int R, bool ACC>
+__global__ void __launch_bounds__(kGfbLdsThreads) gfbit_lds_apply(const GfbArgs<R> a) {
+  constexpr int LW = 2;
+  constexpr int kChunks = W * (int)(kGfbLdsSlice / 16u);          // 16-B chunks per block
+  constexpr int NQ = (kChunks + kGfbLdsThreads - 1) / kGfbLdsThreads;
+  __shared__ u32x4 buf[2][kChunks];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t obj = blockIdx.x / a.tiles;
+  const uint32_t tile = blockIdx.x - obj * a.tiles;
+  const uint32_t t0 = tile * kGfbLdsSlice;
+  const uint32_t off = t0 + tid * 8u;
+  const bool active = off < a.ps;
+  const uint64_t o64 = obj;
+  LaneVec<LW> acc[R][W];
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      if (ACC && active) {
+        const uint32_t pk = (uint32_t)x * a.ps;
+        const uint32_t bv = a.out[i].valid;
+        acc[i][x] = lv_load<LW>(a.out[i].base + o64 * a.out[i].stride + pk, off,
+                                bv > pk ? bv - pk : 0u);
+      } else {
+#pragma unroll
+        for (int e = 0; e < LW; ++e) acc[i][x].v[e] = 0u;
+      }
+    }
+  u32x4 stage[NQ];
+  auto gload = [&](int j) {
+    const uint8_t* base = a.in[j].base + o64 * a.in[j].stride;
+    const uint32_t bv = a.in[j].valid;
+#pragma unroll
+    for (int r = 0; r < NQ; ++r) {
+      const uint32_t q = tid + (uint32_t)r * kGfbLdsThreads;
+      stage[r] = u32x4{0u, 0u, 0u, 0u};
+      if (q < (uint32_t)kChunks) {
+        const uint32_t x = q / (kGfbLdsSlice / 16u);
+        const uint32_t po = t0 + (q % (kGfbLdsSlice / 16u)) * 16u;  // offset inside the packet
+        const uint32_t pk = x * a.ps;
+        uint32_t v = bv > pk ? bv - pk : 0u;  // valid bytes of this packet
+        v = v < a.ps ? v : a.ps;
+        stage[r] = load_guarded(base + pk, po, v);
+      }
+    }
+  };
+  auto swrite = [&](int b) {
+#pragma unroll
+    for (int r = 0; r < NQ; ++r) {
+      const uint32_t q = tid + (uint32_t)r * kGfbLdsThreads;
+      if (q < (uint32_t)kChunks) buf[b][q] = stage[r];
+    }
+  };
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int j = 0; j < a.K; ++j) {
+    const int cur = j & 1;
+    if (j + 1 < a.K) gload(j + 1);
+    LaneVec<LW> y[W];
+    const uint32_t* lb = reinterpret_cast<const uint32_t*>(&buf[cur][0]);
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      typedef uint32_t v2 __attribute__((ext_vector_type(2)));
+      const v2 t = *reinterpret_cast<const v2*>(lb + x * (kGfbLdsSlice / 4u) + tid * 2u);
+      y[x].v[0] = t[0];
+      y[x].v[1] = t[1];
+    }
+    uint32_t c[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) c[i] = a.coef[i][j];
+    gfb_accumulate<W, R, LW, false>(acc, y, c);
+    if (j + 1 < a.K) swrite(cur ^ 1);
+    __syncthreads();
+  }
+  if (!active) return;
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     uint8_t* p = const_cast<uint8_t*>(a.out[i].base) + o64 * a.out[i].stride;

@@ -260,6 +260,8 @@ def test_device_roundtrip_bench_shape(gpu, le):
 @pytest.mark.parametrize("env", [{"LEOEC_BITMATRIX": "1"}, {"LEOEC_GFBIT_LW": "1"},
                                  {"LEOEC_GFBIT_LW": "4"}, {"LEOEC_GFBIT_PF": "0"},
                                  {"LEOEC_GFBIT_PF": "0", "LEOEC_GFBIT_LW": "1"},
+                                 {"LEOEC_GFBIT_LDS": "1"}, {"LEOEC_GFBIT_PF": "2"},
+                                 {"LEOEC_GFBIT_PF": "3", "LEOEC_GFBIT_LW": "1"},
                                  {"LEOEC_BITMATRIX": "1", "LEOEC_BIT_FORM": "0"},
                                  {"LEOEC_BITMATRIX": "1", "LEOEC_BIT_FORM": "1"},
                                  {"LEOEC_BITMATRIX": "1", "LEOEC_BIT_FORM": "2"}],
@@ -278,7 +280,7 @@ def test_cauchy_kernel_forms_agree(gpu, le, oracle, env, monkeypatch):
         assert st == "ok" and out == data
 
 
-@pytest.mark.parametrize("form", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("form", ["0", "1", "2", "3", "4", "5", "6"])
 def test_bitmatrix_kernel_forms_agree(gpu, le, oracle, form, monkeypatch):
     """liberation (and >32 output packets: w = 17 cauchy) through every form of
     the bitmatrix kernel: masked / branchy, with and without look-ahead."""

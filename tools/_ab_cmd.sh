@@ -1,3 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python tools/env_ab.py --variants ";LEOEC_GFBIT_WG=128;LEOEC_GFBIT_WG=512;LEOEC_GFBIT_WG=1024;LEOEC_GFBIT_WG=5121;LEOEC_GFBIT_WG=10241;LEOEC_GFBIT_CEIL=1" > gpurun_out/ab_cauchy3.log 2>&1
+timeout -k 10 1000 python -m pytest tests -x -q -m gpu > gpurun_out/pytest.log 2>&1 || { tail -30 gpurun_out/pytest.log; exit 1; }
+timeout -k 10 900 python tools/bench_suite.py > gpurun_out/suite.log 2>&1

@@ -97,7 +97,7 @@ def main():
         ms = statistics.median(ts)
         alg = ops[o][1]
         print(json.dumps({"config": f"{args.coding}{p}", "variant": v or "default", "op": o,
-                          "ms": round(ms, 4), "alg_GBps": round(alg / ms / 1e6, 1),
+                          "size": args.size, "ms": round(ms, 4), "alg_GBps": round(alg / ms / 1e6, 1),
                           "frac": round(alg / ms / 1e6 / 8000, 4), "correct": ok[v]}), flush=True)
 
 
