@@ -36,8 +36,8 @@ def shard_range(rank, world, total):
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=30)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=100)
     p.add_argument("--objects", type=int, default=1024, help="1 MiB objects per GPU")
     p.add_argument("--size", type=int, default=1048576)
     p.add_argument("--cpu-seconds", type=float, default=12.0,

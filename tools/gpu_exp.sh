@@ -25,7 +25,7 @@ for p in "${PARTS[@]}"; do
       cd /tmp && export TMPDIR=/tmp
       step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu
       step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu
-      step prof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_csv" -o run -- python "$ROOT/bench.py" --steps 10 --no-cpu
+      step prof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_csv" -o run -- python "$ROOT/bench.py" --no-cpu
       cd "$ROOT" ;;
   esac
 done
