@@ -33,10 +33,28 @@ ChunkFn gf16_pick(int r, bool acc) {
   return tbl[acc ? 1 : 0][r - 1];
 }
 
-// LEOEC_GF16_SHIFT=1 selects the shift-and-add kernel for w = 16 (A/B).
-int gf16_pick_env() {
-  const char* e = std::getenv("LEOEC_GF16_SHIFT");
-  return e ? std::atoi(e) : 0;
+// LEOEC_GFW_FORM selects the w = 16 / 32 kernel (A/B measurements):
+//   0 byte-plane v_perm (gfp_apply, shipped)
+//   1 w=16: 2-bit-field v_perm (gf16_apply); w=32: shift-and-add
+//   2 shift-and-add (gfw_apply)
+// LEOEC_GFP_CPT=1|2 sets gfp_apply's 16-byte columns per lane.
+int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
+template <int W>
+ChunkFn gfp_pick(int r, bool acc, int cpt) {
+  static const ChunkFn tbl[2][2][kMaxR] = {
+      {{&launch_gfp_t<W, 1, false, 1>, &launch_gfp_t<W, 2, false, 1>,
+        &launch_gfp_t<W, 3, false, 1>, &launch_gfp_t<W, 4, false, 1>},
+       {&launch_gfp_t<W, 1, true, 1>, &launch_gfp_t<W, 2, true, 1>, &launch_gfp_t<W, 3, true, 1>,
+        &launch_gfp_t<W, 4, true, 1>}},
+      {{&launch_gfp_t<W, 1, false, 2>, &launch_gfp_t<W, 2, false, 2>,
+        &launch_gfp_t<W, 3, false, 2>, &launch_gfp_t<W, 4, false, 2>},
+       {&launch_gfp_t<W, 1, true, 2>, &launch_gfp_t<W, 2, true, 2>, &launch_gfp_t<W, 3, true, 2>,
+        &launch_gfp_t<W, 4, true, 2>}}};
+  return tbl[cpt == 2 ? 1 : 0][acc ? 1 : 0][r - 1];
 }
 
 template <int W>
@@ -104,6 +122,7 @@ int device_cus() {
   }();
   return cus;
 }
+int gfp_blocks_per_cu() { return env_int("LEOEC_GFP_BPC", 64); }
 }  // namespace detail
 
 int launch(const GfApply& p, hipStream_t s) {
@@ -131,10 +150,15 @@ int launch(const GfApply& p, hipStream_t s) {
             const int var = gf8_variant_env();
             if (var > 0 && gf8_variant(var)) fn = gf8_variant(var);
           }
-        } else if (p.w == 16) {
-          fn = gf16_pick_env() ? gfw_pick<16>(nr, j0 > 0) : gf16_pick(nr, j0 > 0);
         } else {
-          fn = gfw_pick<32>(nr, j0 > 0);
+          const int form = env_int("LEOEC_GFW_FORM", 0);
+          const int cpt = env_int("LEOEC_GFP_CPT", 2);
+          if (form == 0)
+            fn = p.w == 16 ? gfp_pick<16>(nr, j0 > 0, cpt) : gfp_pick<32>(nr, j0 > 0, cpt);
+          else if (form == 1 && p.w == 16)
+            fn = gf16_pick(nr, j0 > 0);
+          else
+            fn = p.w == 16 ? gfw_pick<16>(nr, j0 > 0) : gfw_pick<32>(nr, j0 > 0);
         }
         const int rc = fn(p, c, s);
         if (rc) return rc;

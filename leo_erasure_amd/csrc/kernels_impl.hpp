@@ -502,6 +502,199 @@ __global__ void __launch_bounds__(kThreads) gf16_apply(const Gf16Args<R> a) {
 }
 
 // ===========================================================================
+// GF(2^16) / GF(2^32) on byte planes.  Multiplication by c is GF(2)-linear,
+// so byte o of c*x is the XOR over input bytes b of M_ob(x_b), with M_ob(v) =
+// byte o of c*(v << 8b): an 8-bit -> 8-bit linear map, applied exactly like
+// the GF(2^8) kernel applies a coefficient (three v_perm lookups of 8-entry
+// byte tables over the 3/3/2-bit split of v).  A v_perm applies one table to
+// the four bytes of a dword, so a lane's 16-byte column is first transposed
+// into byte planes: plane dword pd = b*G + g holds byte b of four words (G =
+// 4 / NB dwords per plane, NB = W / 8 bytes per word).  Per coefficient and
+// 4 words: NB*NB maps x 3 perms (w=32: 48 perms + 24 xor3; w=16, 8 words:
+// 24 perms + 12 xor3), against 8*W masked xors + doublings for shift-and-add.
+// Coefficients 1 / 0 take a scalar branch (plain xor / skip).  The per-
+// coefficient tables are built in LDS by each workgroup (powers c*x^u, then
+// the table bytes); the grid walks the tiles (grid-stride) so that prologue
+// is paid a few times per CU, not once per tile.
+template <int R>
+struct GfpArgs {
+  DevShard in[kMaxK];
+  DevShard out[R];
+  uint32_t coef[R][kMaxK];
+  int K;
+  uint32_t tiles;        // tiles per object
+  uint32_t vmin;         // min valid over all shards of the launch
+  uint32_t total_tiles;  // tiles of the launch
+};
+
+template <int W, int R>
+struct GfpLds {
+  static constexpr int NB = W / 8, NM = NB * NB, N2 = (NM + 3) / 4;
+  u32x4 t01[R * kMaxK][NM];  // map m = o*NB + b: T0 lo, T0 hi, T1 lo, T1 hi
+  uint32_t t2[R * kMaxK][N2 * 4];  // T2 of map m at [m]
+  uint32_t pw[R * kMaxK][W];       // c * x^u
+};
+
+template <int W>
+__device__ __forceinline__ uint32_t gfw_xtime1(uint32_t v) {
+  if (W == 32) return (v << 1) ^ ((v >> 31) ? 0x00400007u : 0u);
+  return ((v << 1) ^ ((v & 0x8000u) ? 0x1100Bu : 0u)) & 0xFFFFu;
+}
+
+// Byte-plane transposes of one 16-byte column (self-inverse for W = 32).
+template <int W>
+__device__ __forceinline__ u32x4 to_planes(u32x4 x) {
+  if (W == 32) {
+    const uint32_t a0 = perm(x[1], x[0], 0x05010400u), a1 = perm(x[1], x[0], 0x07030602u);
+    const uint32_t b0 = perm(x[3], x[2], 0x05010400u), b1 = perm(x[3], x[2], 0x07030602u);
+    return u32x4{perm(b0, a0, 0x05040100u), perm(b0, a0, 0x07060302u), perm(b1, a1, 0x05040100u),
+                 perm(b1, a1, 0x07060302u)};
+  }
+  // W = 16: [lo g0, lo g1, hi g0, hi g1], group g = words 4g..4g+3
+  return u32x4{perm(x[1], x[0], 0x06040200u), perm(x[3], x[2], 0x06040200u),
+               perm(x[1], x[0], 0x07050301u), perm(x[3], x[2], 0x07050301u)};
+}
+template <int W>
+__device__ __forceinline__ u32x4 from_planes(u32x4 p) {
+  if (W == 32) return to_planes<32>(p);
+  return u32x4{perm(p[2], p[0], 0x05010400u), perm(p[2], p[0], 0x07030602u),
+               perm(p[3], p[1], 0x05010400u), perm(p[3], p[1], 0x07030602u)};
+}
+
+template <int W, int R, bool ACC, int CPT>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))
+gfp_apply(const GfpArgs<R> a) {
+  constexpr int NB = W / 8, G = 4 / NB;
+  constexpr int NM = NB * NB;
+  constexpr uint32_t CS = kTileBytes;
+  constexpr uint32_t TB = CS * CPT;
+  __shared__ GfpLds<W, R> L;
+  const int K = a.K;
+  const int nco = R * K;
+  // prologue 1: powers c * x^u (one thread per coefficient, W serial steps)
+  for (int ci = threadIdx.x; ci < nco; ci += kThreads) {
+    uint32_t v = a.coef[ci / K][ci % K];
+    for (int u = 0; u < W; ++u) {
+      L.pw[ci][u] = v;
+      v = gfw_xtime1<W>(v);
+    }
+  }
+  __syncthreads();
+  // prologue 2: the 20 table bytes of every (coefficient, map)
+  for (int i = threadIdx.x; i < nco * NM; i += kThreads) {
+    const int ci = i / NM, m = i - ci * NM;
+    const int o = m / NB, b = m - o * NB;
+    const uint32_t* pw = &L.pw[ci][8 * b];
+    auto entry = [&](int t0, uint32_t v) {  // byte o of c * ((v << t0) << 8b)
+      uint32_t s = 0;
+      for (int t = 0; t < 3; ++t)
+        if ((v >> t) & 1u) s ^= pw[t0 + t];
+      return (s >> (8 * o)) & 0xFFu;
+    };
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0;
+    for (int e = 0; e < 4; ++e) {
+      w0 |= entry(0, e) << (8 * e);
+      w1 |= entry(0, e + 4) << (8 * e);
+      w2 |= entry(3, e) << (8 * e);
+      w3 |= entry(3, e + 4) << (8 * e);
+      w4 |= entry(6, e) << (8 * e);
+    }
+    L.t01[ci][m] = u32x4{w0, w1, w2, w3};
+    L.t2[ci][m] = w4;
+  }
+  __syncthreads();
+
+  for (uint32_t g = blockIdx.x; g < a.total_tiles; g += gridDim.x) {
+    const uint32_t obj = g / a.tiles;
+    const uint32_t t0 = (g - obj * a.tiles) * TB;
+    const uint32_t off = t0 + threadIdx.x * 16u;
+    const bool full = t0 + TB <= a.vmin;  // wave-uniform
+    const uint64_t o64 = obj;
+    u32x4 acc[R][CPT];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        acc[r][c] = u32x4{0u, 0u, 0u, 0u};
+        if (ACC)
+          acc[r][c] = to_planes<W>(
+              load_guarded(a.out[r].base + o64 * a.out[r].stride, off + c * CS, a.out[r].valid));
+      }
+    auto load = [&](int j, u32x4 (&x)[CPT]) {
+      const uint8_t* p = a.in[j].base + o64 * a.in[j].stride;
+#pragma unroll
+      for (int c = 0; c < CPT; ++c)
+        x[c] = full ? ld16<true>(p + off + c * CS) : load_guarded(p, off + c * CS, a.in[j].valid);
+    };
+    u32x4 nxt[CPT];
+    load(0, nxt);
+    for (int j = 0; j < K; ++j) {
+      u32x4 pl[CPT];
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) pl[c] = to_planes<W>(nxt[c]);
+      if (j + 1 < K) load(j + 1, nxt);
+      uint32_t s0[CPT][4], s1[CPT][4], s2[CPT][4];
+#pragma unroll
+      for (int c = 0; c < CPT; ++c)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          s0[c][d] = pl[c][d] & 0x07070707u;
+          s1[c][d] = (pl[c][d] >> 3) & 0x07070707u;
+          s2[c][d] = (pl[c][d] >> 6) & 0x03030303u;
+        }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint32_t cf = a.coef[r][j];  // wave-uniform
+        if (cf == 0u) continue;
+        if (cf == 1u) {
+#pragma unroll
+          for (int c = 0; c < CPT; ++c) acc[r][c] ^= pl[c];
+          continue;
+        }
+        const int ci = r * K + j;
+#pragma unroll
+        for (int o = 0; o < NB; ++o) {
+          u32x4 t[NB];
+          uint32_t t2[NB];
+#pragma unroll
+          for (int b = 0; b < NB; ++b) {
+            t[b] = L.t01[ci][o * NB + b];
+            t2[b] = L.t2[ci][o * NB + b];
+          }
+#pragma unroll
+          for (int gg = 0; gg < G; ++gg)
+#pragma unroll
+            for (int c = 0; c < CPT; ++c) {
+              uint32_t p[3 * NB];  // 3*NB terms (even), folded pairwise into acc by xor3
+#pragma unroll
+              for (int b = 0; b < NB; ++b) {
+                const int d = b * G + gg;
+                p[3 * b] = perm(t[b][1], t[b][0], s0[c][d]);
+                p[3 * b + 1] = perm(t[b][3], t[b][2], s1[c][d]);
+                p[3 * b + 2] = perm(t2[b], t2[b], s2[c][d]);
+              }
+              uint32_t v = acc[r][c][o * G + gg];
+#pragma unroll
+              for (int q = 0; q < 3 * NB; q += 2) v = xor3(v, p[q], p[q + 1]);
+              acc[r][c][o * G + gg] = v;
+            }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      uint8_t* p = const_cast<uint8_t*>(a.out[r].base) + o64 * a.out[r].stride;
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        const u32x4 v = from_planes<W>(acc[r][c]);
+        if (full) st16<true>(p + off + c * CS, v);
+        else store_guarded(p, off + c * CS, a.out[r].valid, v);
+      }
+    }
+  }
+}
+
+// ===========================================================================
 // Bitmatrix (GF(2)) over packets of ps bytes.
 struct BitArgs {
   DevShard in[kMaxK];
@@ -939,6 +1132,7 @@ inline void gf8_tables(uint32_t c, uint32_t t[5]) {
 }
 
 int device_cus();  // compute units of the current device (kernels.hip)
+int gfp_blocks_per_cu();  // resident-grid size of gfp_apply (kernels.hip)
 
 // BRANCHY = -1: pick per launch from the coefficients (scalar-branch form
 // when enough coefficients are 0/1, the paired all-table form otherwise).
@@ -1029,6 +1223,33 @@ int launch_gf16_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   a.vmin = vmin;
   hipLaunchKernelGGL((gf16_apply<R, ACC>), dim3((uint32_t)(c.no * c.tiles)), dim3(kThreads), 0, s,
                      a);
+  return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
+}
+
+template <int W, int R, bool ACC, int CPT>
+int launch_gfp_t(const GfApply& p, const Chunk& c, hipStream_t s) {
+  GfpArgs<R> a;
+  uint32_t vmin = 0xFFFFFFFFu;
+  a.K = c.nk;
+  for (int j = 0; j < kMaxK; ++j) {
+    a.in[j] = j < c.nk ? dev_shard(p.in[c.j0 + j], c.o0) : DevShard{nullptr, 0, 0, 0};
+    if (j < c.nk) vmin = a.in[j].valid < vmin ? a.in[j].valid : vmin;
+  }
+  for (int r = 0; r < R; ++r) {
+    a.out[r] = dev_shard(p.out[c.r0 + r], c.o0);
+    vmin = a.out[r].valid < vmin ? a.out[r].valid : vmin;
+    for (int j = 0; j < kMaxK; ++j)
+      a.coef[r][j] = j < c.nk ? p.coef[(size_t)(c.r0 + r) * p.K + c.j0 + j] : 0u;
+  }
+  const uint32_t tb = kTileBytes * CPT;
+  a.tiles = (uint32_t)((p.block_size + tb - 1) / tb);
+  a.vmin = vmin;
+  a.total_tiles = (uint32_t)(c.no * a.tiles);
+  // resident-sized grid, every block walking the same number of tiles
+  const uint32_t cap = (uint32_t)device_cus() * gfp_blocks_per_cu();
+  const uint32_t per = (a.total_tiles + cap - 1) / cap;
+  const uint32_t grid = (a.total_tiles + per - 1) / per;
+  hipLaunchKernelGGL((gfp_apply<W, R, ACC, CPT>), dim3(grid), dim3(kThreads), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }
 

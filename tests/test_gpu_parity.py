@@ -324,14 +324,27 @@ def test_file_helpers(gpu, le, tmp_path, monkeypatch):
     assert (tmp_path / "testbin.dec").read_bytes() == data
 
 
-@pytest.mark.parametrize("shift", ["0", "1"])
-def test_gf16_kernel_forms_agree(gpu, le, oracle, shift, monkeypatch):
-    """w = 16 through the v_perm kernel and the shift-and-add kernel."""
-    monkeypatch.setenv("LEOEC_GF16_SHIFT", shift)
-    for k, m in [(10, 4), (4, 2), (17, 5)]:
-        data = rand_bytes(200011, k * m)
-        st, blocks = le.nif_encode("vandrs", (k, m, 16), data, len(data))
-        assert st == "ok" and blocks == oracle.encode("vandrs", k, m, 16, data)
+@pytest.mark.parametrize("w", [16, 32])
+@pytest.mark.parametrize("env", [
+    {},                                        # shipped: byte-plane v_perm, 2 columns per lane
+    {"LEOEC_GFP_CPT": "1"},                    # byte-plane, 1 column per lane
+    {"LEOEC_GFP_BPC": "1"},                    # byte-plane, 1 block per CU: long grid-stride walks
+    {"LEOEC_GFW_FORM": "1"},                   # w=16: 2-bit-field v_perm; w=32: shift-and-add
+    {"LEOEC_GFW_FORM": "2"},                   # shift-and-add
+])
+def test_gfw_kernel_forms_agree(gpu, le, oracle, w, env, monkeypatch):
+    """w = 16 / 32 through every kernel form: encode vs the oracle, decode
+    and repair round trips, including > 16 inputs (accumulating launches,
+    whose outputs are re-read into byte planes) and ragged tails."""
+    for key, val in env.items():
+        monkeypatch.setenv(key, val)
+    for k, m, size in [(10, 4, 200011), (4, 2, 77777), (17, 5, 123457), (3, 3, 1000)]:
+        data = rand_bytes(size, k * m + w)
+        st, blocks = le.nif_encode("vandrs", (k, m, w), data, len(data))
+        assert st == "ok" and blocks == oracle.encode("vandrs", k, m, w, data)
         ids = list(range(m, k + m))
-        st, out = le.nif_decode("vandrs", (k, m, 16), [blocks[i] for i in ids], ids, len(data))
+        st, out = le.nif_decode("vandrs", (k, m, w), [blocks[i] for i in ids], ids, len(data))
         assert st == "ok" and out == data
+        ids = list(range(1, k + 1))
+        st, rep = le.nif_repair("vandrs", (k, m, w), [blocks[i] for i in ids], ids, [0, k + m - 1])
+        assert st == "ok" and rep == [blocks[0], blocks[k + m - 1]]
