@@ -123,6 +123,8 @@ int device_cus() {
   return cus;
 }
 int gfp_blocks_per_cu() { return env_int("LEOEC_GFP_BPC", 64); }
+// LEOEC_GF8_TMAP: gf8_apply workgroup -> tile order (Gf8Args::tmap), A/B only.
+int gf8_tile_map() { return env_int("LEOEC_GF8_TMAP", 0); }
 }  // namespace detail
 
 int launch(const GfApply& p, hipStream_t s) {

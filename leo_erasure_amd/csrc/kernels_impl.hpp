@@ -124,6 +124,10 @@ struct Gf8Args {
   uint32_t tiles;         // tiles per object
   uint32_t vmin;          // min valid over all shards of the launch
   uint32_t total_tiles;   // tiles of the launch (persistent form)
+  uint32_t nobj;          // objects of the launch
+  uint32_t tmap;          // workgroup -> tile order: 0 tile-major, 1 object-major,
+                          // 2 tiles of an object visited with stride tperm (coprime)
+  uint32_t tperm;
 };
 
 // Kernel shape / policy knobs (the engine ships kGf8Default; the others exist
@@ -307,8 +311,15 @@ gf8_apply(const Gf8Args<K, R> a) {
   }
   if (!PIPE) {
     const uint32_t b = XMAP ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t obj = b / a.tiles;
-    const uint32_t tile = b - obj * a.tiles;
+    uint32_t obj, tile;
+    if (a.tmap == 1) {
+      tile = b / a.nobj;
+      obj = b - tile * a.nobj;
+    } else {
+      obj = b / a.tiles;
+      tile = b - obj * a.tiles;
+      if (a.tmap == 2) tile = (uint32_t)(((uint64_t)tile * a.tperm) % a.tiles);
+    }
     const uint32_t t0 = tile * TB;
     const uint32_t off = t0 + threadIdx.x * 16u;
     const bool full = t0 + TB <= a.vmin;  // wave-uniform
@@ -1133,6 +1144,7 @@ inline void gf8_tables(uint32_t c, uint32_t t[5]) {
 
 int device_cus();  // compute units of the current device (kernels.hip)
 int gfp_blocks_per_cu();  // resident-grid size of gfp_apply (kernels.hip)
+int gf8_tile_map();       // gf8_apply workgroup -> tile order (kernels.hip)
 
 // BRANCHY = -1: pick per launch from the coefficients (scalar-branch form
 // when enough coefficients are 0/1, the paired all-table form otherwise).
@@ -1164,6 +1176,15 @@ int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   a.tiles = (uint32_t)((p.block_size + tb - 1) / tb);
   a.vmin = vmin;
   a.total_tiles = (uint32_t)(c.no * a.tiles);
+  a.nobj = (uint32_t)c.no;
+  a.tmap = (uint32_t)gf8_tile_map();
+  a.tperm = 1;
+  if (a.tmap == 2) {  // stride ~ tiles / 16, coprime with tiles (a bijection on tiles)
+    uint32_t q = a.tiles / 16u + 1u;
+    auto gcd = [](uint32_t x, uint32_t y) { while (y) { const uint32_t t = x % y; x = y; y = t; } return x; };
+    while (gcd(q, a.tiles) != 1u) ++q;
+    a.tperm = q % a.tiles ? q % a.tiles : 1u;
+  }
   // per-dword VALU: general coefficient 5.5 (branchy) vs 5 (paired); a 1 costs
   // 1 and a 0 nothing in the branchy form
   const int n = R * K;

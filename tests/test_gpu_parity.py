@@ -348,3 +348,78 @@ def test_gfw_kernel_forms_agree(gpu, le, oracle, w, env, monkeypatch):
         ids = list(range(1, k + 1))
         st, rep = le.nif_repair("vandrs", (k, m, w), [blocks[i] for i in ids], ids, [0, k + m - 1])
         assert st == "ok" and rep == [blocks[0], blocks[k + m - 1]]
+
+
+def test_device_64MiB_objects(gpu, le, oracle):
+    """BASELINE configs[4] geometry: RS(10,4,8) on 64 MiB objects (bs =
+    6,710,912, 256 B of zero pad in block 9), device-resident batch.  Parity of
+    two objects against the oracle, then the size-independent round trips:
+    in-place decode of {0,1,2,3} and repair of a data+parity mix."""
+    k, m, w = 10, 4, 8
+    n, size = 3, 64 * 1024 * 1024
+    bs, _ = le.layout("vandrs", (k, m, w), size)
+    assert bs == 6710912
+    g = gpu.Generator(device="cuda").manual_seed(0x64)
+    objs = gpu.randint(0, 256, (n, size), dtype=gpu.uint8, device="cuda", generator=g)
+    parity = gpu.empty((n, m * bs), dtype=gpu.uint8, device="cuda")
+    le.device.encode("vandrs", (k, m, w), objs, size, parity)
+    gpu.cuda.synchronize()
+    for o in (0, n - 1):
+        ref = oracle.encode("vandrs", k, m, w, objs[o].cpu().numpy().tobytes())
+        assert parity[o].cpu().numpy().tobytes() == b"".join(ref[k:]), f"object {o}"
+    ref = objs.clone()
+    objs[:, : 4 * bs] = 0x5A
+    le.device.decode("vandrs", (k, m, w), objs, size, parity, [0, 1, 2, 3])
+    assert gpu.equal(objs, ref)
+    # repair {0, 5, 10, 13} from the other ten blocks, as separate shards
+    pad = gpu.zeros((n, k * bs), dtype=gpu.uint8, device="cuda")
+    pad[:, :size] = objs
+    blocks = [pad[:, b * bs:(b + 1) * bs] if b < k else parity[:, (b - k) * bs:(b - k + 1) * bs]
+              for b in range(k + m)]
+    blocks = [b.contiguous() for b in blocks]
+    lost = [0, 5, 10, 13]
+    avail = [None if b in lost else blocks[b] for b in range(k + m)]
+    out = [gpu.empty((n, bs), dtype=gpu.uint8, device="cuda") for _ in lost]
+    le.device.repair("vandrs", (k, m, w), avail, bs, lost, out, n)
+    gpu.cuda.synchronize()
+    for r, b in enumerate(lost):
+        assert gpu.equal(out[r], blocks[b]), b
+
+
+def test_concurrent_callers(gpu, le, oracle):
+    """The NIF is callable from any scheduler thread at once (basho_bench t4,
+    test/basho_bench_leo_erasure_rs_10_4_8_1M_w_t4.config): 8 threads each
+    run encode / decode / repair of their own objects through the C ABI
+    (ctypes drops the GIL), over every class; all results match the oracle."""
+    import concurrent.futures as cf
+
+    cases = [("vandrs", 10, 4, 8), ("cauchyrs", 10, 4, 8), ("isars", 10, 4, 8),
+             ("liberation", 4, 2, 7), ("vandrs", 4, 2, 16), ("vandrs", 6, 3, 32)]
+    expect = {}
+    for i, (cls, k, m, w) in enumerate(cases):
+        data = rand_bytes(1048576 + 333 * i, 500 + i)
+        expect[i] = (data, oracle.encode(cls, k, m, w, data))
+
+    def worker(t):
+        for r in range(6):
+            i = (t + r) % len(cases)
+            cls, k, m, w = cases[i]
+            data, ref = expect[i]
+            st, blocks = le.nif_encode(cls, (k, m, w), data, len(data))
+            if st != "ok" or blocks != ref:
+                return f"encode {cls}{(k, m, w)} thread {t}"
+            ids = list(range(m, k + m))[::-1]
+            st, out = le.nif_decode(cls, (k, m, w), [ref[b] for b in ids], ids, len(data))
+            if st != "ok" or out != data:
+                return f"decode {cls}{(k, m, w)} thread {t}"
+            lost = [t % (k + m), (t + 3) % (k + m)]
+            lost = sorted(set(lost))
+            avail = [b for b in range(k + m) if b not in lost]
+            st, rep = le.nif_repair(cls, (k, m, w), [ref[b] for b in avail], avail, lost)
+            if st != "ok" or rep != [ref[b] for b in lost]:
+                return f"repair {cls}{(k, m, w)} {lost} thread {t}"
+        return None
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        errs = [e for e in ex.map(worker, range(8)) if e]
+    assert not errs, errs

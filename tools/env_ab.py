@@ -31,6 +31,10 @@ def main():
     ap.add_argument("--variants", default="")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--par-offset", type=int, default=0,
+                    help="bytes (multiple of 16) the parity rows start past their allocation's base")
+    ap.add_argument("--obj-pad", type=int, default=0,
+                    help="extra bytes (multiple of 16) per object row beyond max(k, m) * block size")
     args = ap.parse_args()
     import torch
     import leo_erasure_amd as le
@@ -40,10 +44,11 @@ def main():
     p = (k, m, w)
     bs, _ = le.layout(args.coding, p, args.size)
     n = args.objects
-    stride = max(k, m) * bs
+    stride = max(k, m) * bs + args.obj_pad
     objs = torch.zeros((n, stride), dtype=torch.uint8, device="cuda")
     objs[:, :args.size].random_(0, 256)
-    par = torch.zeros((n, stride), dtype=torch.uint8, device="cuda")
+    par_buf = torch.zeros(n * stride + args.par_offset, dtype=torch.uint8, device="cuda")
+    par = par_buf[args.par_offset:].view(n, stride)
     ref = objs[:, :args.size].clone()
     er = [int(x) for x in args.erased.split(",") if x]
     e = len([x for x in er if x < k])
@@ -97,6 +102,7 @@ def main():
         ms = statistics.median(ts)
         alg = ops[o][1]
         print(json.dumps({"config": f"{args.coding}{p}", "variant": v or "default", "op": o,
+                          "par_offset": args.par_offset, "obj_pad": args.obj_pad,
                           "size": args.size, "ms": round(ms, 4), "alg_GBps": round(alg / ms / 1e6, 1),
                           "frac": round(alg / ms / 1e6 / 8000, 4), "correct": ok[v]}), flush=True)
 
