@@ -74,12 +74,13 @@ ChunkFn gfw_pick(int r, bool acc) {
 //   2 branchy, no look-ahead       3 branchy, 1 packet ahead
 //   4/5/6 masked, 2/3/5 packets ahead (4 = shipped)
 //   7 as 4, with all tiles of an object on one XCD
+//   8 as 4, output packets padded to 8 / 16 / 32 (4 pads to even)
 // Measured on liberation(7,2,7): masked beats branchy (the scalar branches
 // cost more than the masked xors they save); look-ahead depth see DESIGN.md.
 int bit_form_env() {
   const char* e = std::getenv("LEOEC_BIT_FORM");
   const int f = e ? std::atoi(e) : 4;
-  return (f >= 0 && f <= 7) ? f : 4;
+  return (f >= 0 && f <= 8) ? f : 4;
 }
 
 using BitFn = void (*)(const detail::BitArgs);
@@ -102,6 +103,17 @@ BitFn bit_kernel(int ro, bool acc, int form) {
   if (ro == 8) return acc ? bit_kernel_f<8, true>(form) : bit_kernel_f<8, false>(form);
   if (ro == 16) return acc ? bit_kernel_f<16, true>(form) : bit_kernel_f<16, false>(form);
   return acc ? bit_kernel_f<32, true>(form) : bit_kernel_f<32, false>(form);
+}
+
+// Shipped form with the output-packet count rounded up to even only (2..32):
+// liberation(k,2,w) has 2w output packets (14 at w=7, 22 at w=11), which the
+// {8,16,32} instances pad by up to 45 % of masked xors.
+template <std::size_t... I>
+BitFn bit_kernel_even(std::index_sequence<I...>, int rp, bool acc) {
+  static const BitFn tbl[2][sizeof...(I)] = {
+      {&detail::bit_apply<2 * ((int)I + 1), false, false, 2>...},
+      {&detail::bit_apply<2 * ((int)I + 1), true, false, 2>...}};
+  return tbl[acc ? 1 : 0][(rp + 1) / 2 - 1];
 }
 
 int gf8_variant_env() {
@@ -219,7 +231,10 @@ int launch(const BitApply& p, hipStream_t s) {
         const dim3 grid((uint32_t)(no * tiles)), block(kThreads);
         const int form = bit_form_env();
         const int ro = RP <= 8 ? 8 : RP <= 16 ? 16 : 32;
-        hipLaunchKernelGGL(bit_kernel(ro, acc, form), grid, block, 0, s, a);
+        // LEOEC_BIT_FORM=8: the shipped form at the {8,16,32} sizes (A/B)
+        const BitFn fn = form == 4 ? bit_kernel_even(std::make_index_sequence<16>{}, RP, acc)
+                                   : bit_kernel(ro, acc, form == 8 ? 4 : form);
+        hipLaunchKernelGGL(fn, grid, block, 0, s, a);
         if (hipGetLastError() != hipSuccess) return LEOEC_E_HIP;
       }
     }

@@ -280,7 +280,7 @@ def test_cauchy_kernel_forms_agree(gpu, le, oracle, env, monkeypatch):
         assert st == "ok" and out == data
 
 
-@pytest.mark.parametrize("form", ["0", "1", "2", "3", "4", "5", "6"])
+@pytest.mark.parametrize("form", ["0", "1", "2", "3", "4", "5", "6", "7", "8"])
 def test_bitmatrix_kernel_forms_agree(gpu, le, oracle, form, monkeypatch):
     """liberation (and >32 output packets: w = 17 cauchy) through every form of
     the bitmatrix kernel: masked / branchy, with and without look-ahead."""
