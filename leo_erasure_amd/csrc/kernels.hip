@@ -121,6 +121,75 @@ int gf8_variant_env() {
   return e ? std::atoi(e) : 0;
 }
 
+// True when the plan is exactly a liberation encode bitmatrix (the structure
+// lib_apply<W> compiles in, kernels_impl.hpp): RB = 2, KB <= w, and bit
+// (o, j*w + x) set iff o = x (P), or o = w + (x - j) mod w (Q), or, for
+// j > 0, o = w + y with y = j (w-1)/2 mod w and x = (y + j - 1) mod w.
+bool is_liberation_encode(const BitApply& p) {
+  const int w = p.w, k = p.KB;
+  if (p.RB != 2 || k > w || k > kMaxK) return false;
+  const size_t cols = (size_t)k * w;
+  for (int j = 0; j < k; ++j) {
+    const int y = (j * ((w - 1) / 2)) % w;
+    for (int x = 0; x < w; ++x)
+      for (int o = 0; o < 2 * w; ++o) {
+        bool want = (o == x) || (o == w + (x - j + w) % w);
+        if (j > 0 && o == w + y && x == (y + j - 1) % w) want = true;
+        if ((p.bits[(size_t)o * cols + (size_t)j * w + x] != 0) != want) return false;
+      }
+  }
+  return true;
+}
+
+// LEOEC_LIB_FORM=0 routes liberation encodes through the generic masked
+// bitmatrix kernel (A/B and parity of both forms); default 1 = lib_apply.
+// LEOEC_LIB_LA=2|4|8 sets lib_apply's packet look-ahead (A/B; default 2:
+// profiles/r01_v13_ab_lib_la.log, best or within 1 % of best for w = 5..13).
+using LibFn = void (*)(const detail::LibArgs);
+template <int W>
+LibFn lib_kernel_w(int la) {
+  if (la == 4) return &detail::lib_apply<W, 4>;
+  if (la == 8) return &detail::lib_apply<W, 8>;
+  return &detail::lib_apply<W, 2>;
+}
+LibFn lib_kernel(int w) {
+  const int la = env_int("LEOEC_LIB_LA", 2);
+  switch (w) {
+    case 3: return lib_kernel_w<3>(la);
+    case 5: return lib_kernel_w<5>(la);
+    case 7: return lib_kernel_w<7>(la);
+    case 11: return lib_kernel_w<11>(la);
+    case 13: return lib_kernel_w<13>(la);
+    default: return nullptr;
+  }
+}
+
+int launch_lib(const BitApply& p, LibFn fn, hipStream_t s) {
+  const uint32_t ps = (uint32_t)(p.block_size / (uint64_t)p.w);
+  const uint32_t tiles = (ps + kTileBytes - 1) / kTileBytes;
+  const uint64_t max_obj = (uint64_t)0x7FFFFFFF / tiles;
+  for (uint64_t o0 = 0; o0 < p.nobj; o0 += max_obj) {
+    const uint64_t no = (p.nobj - o0 < max_obj) ? p.nobj - o0 : max_obj;
+    LibArgs a;
+    a.k = p.KB;
+    a.ps = ps;
+    a.tiles = tiles;
+    uint32_t vmin = 0xFFFFFFFFu;
+    for (int j = 0; j < kMaxK; ++j) {
+      a.in[j] = j < p.KB ? dev_shard(p.in[j], o0) : DevShard{nullptr, 0, 0, 0};
+      if (j < p.KB && a.in[j].valid < vmin) vmin = a.in[j].valid;
+    }
+    for (int r = 0; r < 2; ++r) {
+      a.out[r] = dev_shard(p.out[r], o0);
+      if (a.out[r].valid < vmin) vmin = a.out[r].valid;
+    }
+    a.vmin = vmin;
+    hipLaunchKernelGGL(fn, dim3((uint32_t)(no * tiles)), dim3(kThreads), 0, s, a);
+    if (hipGetLastError() != hipSuccess) return LEOEC_E_HIP;
+  }
+  return LEOEC_OK;
+}
+
 }  // namespace
 
 namespace detail {
@@ -190,6 +259,9 @@ int launch(const BitApply& p, hipStream_t s) {
   if (p.block_size == 0 || p.nobj == 0) return LEOEC_OK;
   if (p.block_size % ((uint64_t)16 * w) || p.block_size >= (1ull << 32)) return LEOEC_E_BAD_SIZE;
   if (!shards_ok(p.in) || !shards_ok(p.out)) return LEOEC_E_ARG;
+  if (env_int("LEOEC_LIB_FORM", 1) != 0)
+    if (const LibFn lf = lib_kernel(w))
+      if (is_liberation_encode(p)) return launch_lib(p, lf, s);
   const uint32_t ps = (uint32_t)(p.block_size / (uint64_t)w);
   const uint32_t tiles = (ps + kTileBytes - 1) / kTileBytes;
   const uint64_t max_obj = (uint64_t)0x7FFFFFFF / tiles;

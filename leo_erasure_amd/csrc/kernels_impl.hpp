@@ -79,6 +79,13 @@ __device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
   else *reinterpret_cast<u32x4*>(p) = v;
 }
 
+// Raw buffer resource over [p, p + 4 GiB): loads/stores then take one shared
+// 32-bit VGPR offset plus a per-block SGPR base instead of a 64-bit VGPR
+// address per access (gfx9 dword3 = 0x00020000).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0xFFFFFFFF, 0x00020000);
+}
+
 // Bytes of v at index >= n (0 <= n < 16) cleared.
 __device__ __forceinline__ u32x4 keep_first(u32x4 v, uint32_t n) {
 #pragma unroll
@@ -224,11 +231,19 @@ __device__ __forceinline__ void gf8_tile(const Gf8Args<K, R>& a, const Gf8Lds<K,
   }
 }
 
-template <int K, int R, int CPT, bool NT, uint32_t CS = kTileBytes>
+template <int K, int R, int CPT, bool NT, uint32_t CS = kTileBytes, bool BUF = false>
 __device__ __forceinline__ void gf8_load(const Gf8Args<K, R>& a, uint64_t o, uint32_t off,
                                          bool full, u32x4 (&d)[CPT][K]) {
   constexpr uint32_t kTileBytes = CS;
-  if (full) {
+  if (full && BUF) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const auto rs = buf_rsrc(a.in[j].base + o * a.in[j].stride);
+#pragma unroll
+      for (int c = 0; c < CPT; ++c)
+        d[c][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + c * kTileBytes, 0, NT ? 2 : 0);
+    }
+  } else if (full) {
 #pragma unroll
     for (int j = 0; j < K; ++j)
 #pragma unroll
@@ -259,11 +274,19 @@ __device__ __forceinline__ void gf8_init_store(const Gf8Args<K, R>& a, uint64_t 
     }
 }
 
-template <int K, int R, int CPT, bool NT, uint32_t CS = kTileBytes>
+template <int K, int R, int CPT, bool NT, uint32_t CS = kTileBytes, bool BUF = false>
 __device__ __forceinline__ void gf8_store(const Gf8Args<K, R>& a, uint64_t o, uint32_t off,
                                           bool full, const u32x4 (&acc)[CPT][R]) {
   constexpr uint32_t kTileBytes = CS;
-  if (full) {
+  if (full && BUF) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const auto rs = buf_rsrc(a.out[r].base + o * a.out[r].stride);
+#pragma unroll
+      for (int c = 0; c < CPT; ++c)
+        __builtin_amdgcn_raw_buffer_store_b128(acc[c][r], rs, off + c * kTileBytes, 0, NT ? 2 : 0);
+    }
+  } else if (full) {
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -295,7 +318,7 @@ __device__ __forceinline__ uint32_t xcd_group(uint32_t b, uint32_t n) {
 // that walks the tiles and issues the loads of its next tile before
 // computing the current one (PIPE = true).
 template <int K, int R, bool ACC, int CPT, bool NT, bool BRANCHY, bool COPY, bool PIPE, bool LDS,
-          int WAVES, int WG, bool XMAP>
+          int WAVES, int WG, bool XMAP, bool BUF = false>
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 gf8_apply(const Gf8Args<K, R> a) {
   constexpr uint32_t CS = (uint32_t)WG * 16u;  // bytes of one column group
@@ -324,11 +347,11 @@ gf8_apply(const Gf8Args<K, R> a) {
     const uint32_t off = t0 + threadIdx.x * 16u;
     const bool full = t0 + TB <= a.vmin;  // wave-uniform
     u32x4 d[CPT][K];
-    gf8_load<K, R, CPT, NT, CS>(a, obj, off, full, d);
+    gf8_load<K, R, CPT, NT, CS, BUF>(a, obj, off, full, d);
     u32x4 acc[CPT][R];
     gf8_init_store<K, R, ACC, CPT, NT, CS>(a, obj, off, acc);
     gf8_tile<K, R, CPT, BRANCHY, COPY, LDS>(a, lds, d, acc);
-    gf8_store<K, R, CPT, NT, CS>(a, obj, off, full, acc);
+    gf8_store<K, R, CPT, NT, CS, BUF>(a, obj, off, full, acc);
     return;
   }
   const uint32_t total = a.total_tiles;
@@ -779,6 +802,90 @@ __global__ void __launch_bounds__(kThreads) bit_apply(const BitArgs a) {
 }
 
 // ===========================================================================
+// Liberation encode (m = 2, k <= w, w prime): the bitmatrix of
+// liberation_coding_bitmatrix (codes.cpp; SURVEY Appendix A.4,
+// c_src/liberationcoding.cpp:39) has 2kw + k - 1 ones out of 2kw * w, so the
+// masked kernel above spends ~93 % of its xors on zero bits.  Here the
+// structure is compiled in: with the block index j unrolled (k <= W),
+//   P[x]             ^= D(j, x)
+//   Q[(x - j) mod W] ^= D(j, x)
+//   Q[y]             ^= D(j, (y + j - 1) mod W),  y = j (W - 1) / 2 mod W, j > 0
+// all with static register indices: 2 (or 3) xors per input packet dword,
+// no branches.  The launcher checks the plan's bits against this structure
+// and uses the generic kernel otherwise.  Packets are applied in (j, x) order
+// with the loads of the next LA packets in flight (a ring of registers).
+struct LibArgs {
+  DevShard in[kMaxK];
+  DevShard out[2];  // coding blocks P, Q (base at the block)
+  int k;
+  uint32_t ps;      // packet bytes
+  uint32_t tiles;   // tiles per object (over one packet)
+  uint32_t vmin;    // min valid over inputs and outputs
+};
+
+// Register budget: the 2W accumulators plus the ring; without a bound the
+// scheduler hoists every load of the unrolled body (up to 256 VGPRs, one
+// wave per SIMD).
+constexpr int lib_waves(int w) { return w <= 7 ? 4 : w <= 11 ? 3 : 2; }
+
+template <int W, int LA>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(lib_waves(W), 8)))
+lib_apply(const LibArgs a) {
+  constexpr int RS = LA + 1;  // ring of packet registers: LA loads in flight
+  const uint32_t obj = blockIdx.x / a.tiles;
+  const uint32_t tile = blockIdx.x - obj * a.tiles;
+  const uint32_t t0 = tile * kTileBytes;
+  const uint32_t off = t0 + threadIdx.x * 16u;
+  if (off >= a.ps) return;
+  const uint64_t o64 = obj;
+  // wave-uniform: the tile lies inside the packet and inside every shard's
+  // valid bytes (the last packet of a block is the furthest)
+  const bool full = t0 + kTileBytes <= a.ps &&
+                    (uint64_t)(W - 1) * a.ps + t0 + kTileBytes <= (uint64_t)a.vmin;
+  auto load = [&](int j, int x) {
+    const uint8_t* b = a.in[j].base + o64 * a.in[j].stride;
+    const uint32_t pk = (uint32_t)x * a.ps;
+    if (full) return ld16<true>(b + pk + off);
+    const uint32_t v = a.in[j].valid;
+    return load_guarded(b + pk, off, v > pk ? v - pk : 0u);
+  };
+  u32x4 P[W], Q[W], ring[RS];
+#pragma unroll
+  for (int x = 0; x < W; ++x) P[x] = Q[x] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int q = 0; q < LA; ++q) {
+    ring[q] = u32x4{0u, 0u, 0u, 0u};
+    if (q < W * W && q / W < a.k) ring[q] = load(q / W, q % W);
+  }
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    if (j >= a.k) break;
+    const int y = (j * ((W - 1) / 2)) % W;  // Q row of block j's extra one
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const int p = j * W + x, q = p + LA;  // packet applied / packet loaded
+      if (q < W * W && q / W < a.k) ring[q % RS] = load(q / W, q % W);
+      const u32x4 v = ring[p % RS];
+      P[x] ^= v;
+      Q[(x - j + W) % W] ^= v;
+      if (j > 0 && x == (y + j - 1) % W) Q[y] ^= v;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    uint8_t* b = const_cast<uint8_t*>(a.out[r].base) + o64 * a.out[r].stride;
+    const uint32_t v = a.out[r].valid;
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const uint32_t pk = (uint32_t)x * a.ps;
+      const u32x4 acc = r == 0 ? P[x] : Q[x];
+      if (full) st16<true>(b + pk + off, acc);
+      else store_guarded(b + pk, off, v > pk ? v - pk : 0u, acc);
+    }
+  }
+}
+
+// ===========================================================================
 // GF(2^w) on packet-bitsliced blocks (cauchyrs).  Each lane owns LW dwords of
 // every packet.  Per input block: y = its w packets; for t = 0..w-1, every
 // output block whose coefficient has bit t set gets y xor-ed in, then
@@ -1151,7 +1258,7 @@ int gf8_tile_map();       // gf8_apply workgroup -> tile order (kernels.hip)
 template <int K, int R, bool ACC, int CPT = kGf8Default.cpt, bool NT = kGf8Default.nt,
           int BRANCHY = kGf8Default.branchy, bool COPY = kGf8Default.copy, bool PIPE = false,
           bool LDS = kGf8Default.lds, int WAVES = kGf8Default.waves, int WG = kThreads,
-          bool XMAP = false>
+          bool XMAP = false, bool BUF = false>
 int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   Gf8Args<K, R> a;
   a.one = a.zero = 0;
@@ -1195,10 +1302,10 @@ int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
     grid = grid < cap ? grid : cap;
   }
   if (branchy)
-    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, true, COPY, PIPE, LDS, WAVES, WG, XMAP>),
+    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, true, COPY, PIPE, LDS, WAVES, WG, XMAP, BUF>),
                        dim3(grid), dim3(WG), 0, s, a);
   else
-    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, false, COPY, PIPE, LDS, WAVES, WG, XMAP>),
+    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, false, COPY, PIPE, LDS, WAVES, WG, XMAP, BUF>),
                        dim3(grid), dim3(WG), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }

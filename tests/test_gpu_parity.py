@@ -297,6 +297,47 @@ def test_bitmatrix_kernel_forms_agree(gpu, le, oracle, form, monkeypatch):
         assert st == "ok" and rep == [blocks[0], blocks[k]]
 
 
+@pytest.mark.parametrize("form", ["0", "1"])
+def test_liberation_encode_forms(gpu, le, oracle, form, monkeypatch):
+    """lib_apply (the liberation bitmatrix structure compiled in, LEOEC_LIB_FORM=1,
+    shipped) and the generic masked bitmatrix kernel (0): every instantiated w,
+    k from 1 to w, sizes with ragged tails, against the oracle; decode and
+    repair (generic kernel) of what was encoded."""
+    monkeypatch.setenv("LEOEC_LIB_FORM", form)
+    for w in (3, 5, 7, 11, 13):
+        for k in sorted({1, 2, (w + 1) // 2, w}):
+            for size in (1, 4097, 150001):
+                data = rand_bytes(size, k * 100 + w + size)
+                st, blocks = le.nif_encode("liberation", (k, 2, w), data, size)
+                assert st == "ok", blocks
+                assert blocks == oracle.encode("liberation", k, 2, w, data), (k, w, size)
+            ids = list(range(2, k + 2))
+            st, out = le.nif_decode("liberation", (k, 2, w), [blocks[i] for i in ids], ids, size)
+            assert st == "ok" and out == data, (k, w)
+            st, rep = le.nif_repair("liberation", (k, 2, w), [blocks[i] for i in ids], ids, [0, k, k + 1])
+            assert st == "ok" and rep == [blocks[0], blocks[k], blocks[k + 1]], (k, w)
+
+
+def test_liberation_device_batch_forms(gpu, le, oracle, monkeypatch):
+    """Device-resident batch (ragged object size, 37 objects) through both
+    liberation encode forms: identical parity, equal to the oracle."""
+    k, m, w = 7, 2, 7
+    n, size = 37, 300007
+    bs, _ = le.layout("liberation", (k, m, w), size)
+    host, objs = _batch(gpu, n, size, size + 9 - (size + 9) % 16 + 16, 21)
+    outs = []
+    for form in ("1", "0"):
+        monkeypatch.setenv("LEOEC_LIB_FORM", form)
+        parity = gpu.full((n, m * bs), 0x5A, dtype=gpu.uint8, device="cuda")
+        le.device.encode("liberation", (k, m, w), objs, size, parity)
+        gpu.cuda.synchronize()
+        outs.append(parity.cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    for o in range(0, n, 6):
+        ref = oracle.encode("liberation", k, m, w, host[o, :size].tobytes())
+        assert outs[0][o].tobytes() == b"".join(ref[k:]), f"object {o}"
+
+
 def test_golden_fixtures_gpu(gpu, le):
     """The committed restatement-derived fixtures, through the GPU engine."""
     import json
