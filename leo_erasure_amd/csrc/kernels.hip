@@ -206,6 +206,7 @@ int device_cus() {
 int gfp_blocks_per_cu() { return env_int("LEOEC_GFP_BPC", 64); }
 // LEOEC_GF8_TMAP: gf8_apply workgroup -> tile order (Gf8Args::tmap), A/B only.
 int gf8_tile_map() { return env_int("LEOEC_GF8_TMAP", 0); }
+int gf8_wg_env() { return env_int("LEOEC_GF8_WG", 0); }
 }  // namespace detail
 
 int launch(const GfApply& p, hipStream_t s) {
@@ -217,7 +218,9 @@ int launch(const GfApply& p, hipStream_t s) {
   if ((p.block_size & 15u) || p.block_size >= (1ull << 32)) return LEOEC_E_BAD_SIZE;
   if (!shards_ok(p.in) || !shards_ok(p.out)) return LEOEC_E_ARG;
   const uint32_t tiles = (uint32_t)((p.block_size + kTileBytes - 1) / kTileBytes);
-  const uint64_t max_obj = (uint64_t)0x7FFFFFFF / tiles;
+  // objects per launch bounded for the narrowest tiles (1 KiB, gf8_apply's
+  // 64-lane form) so no grid exceeds 2^31 - 1 workgroups
+  const uint64_t max_obj = (uint64_t)0x7FFFFFFF / ((p.block_size + 1023) / 1024);
   for (uint64_t o0 = 0; o0 < p.nobj; o0 += max_obj) {
     const uint64_t no = (p.nobj - o0 < max_obj) ? p.nobj - o0 : max_obj;
     for (int r0 = 0; r0 < p.R; r0 += kMaxR) {

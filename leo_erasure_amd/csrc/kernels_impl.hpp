@@ -323,9 +323,13 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(WAVES, 
 gf8_apply(const Gf8Args<K, R> a) {
   constexpr uint32_t CS = (uint32_t)WG * 16u;  // bytes of one column group
   constexpr uint32_t TB = CS * CPT;
+  // With one column per lane the launcher may use fewer lanes than WG (the
+  // workgroup size is then the tile width: 64 lanes = 1 KiB tiles, chosen for
+  // large blocks); CPT > 1 forms always launch WG lanes.
+  const uint32_t TBr = CPT == 1 ? blockDim.x * 16u : TB;
   __shared__ Gf8Lds<K, R> lds;
   if (LDS) {
-    for (uint32_t i = threadIdx.x; i < (uint32_t)(R * K); i += WG) {
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(R * K); i += blockDim.x) {
       const uint32_t* t = a.tab[i / K][i % K];
       lds.t[i][0] = u32x4{t[0], t[1], t[2], t[3]};
       lds.t[i][1] = u32x4{t[4], 0u, 0u, 0u};
@@ -343,9 +347,9 @@ gf8_apply(const Gf8Args<K, R> a) {
       tile = b - obj * a.tiles;
       if (a.tmap == 2) tile = (uint32_t)(((uint64_t)tile * a.tperm) % a.tiles);
     }
-    const uint32_t t0 = tile * TB;
+    const uint32_t t0 = tile * TBr;
     const uint32_t off = t0 + threadIdx.x * 16u;
-    const bool full = t0 + TB <= a.vmin;  // wave-uniform
+    const bool full = t0 + TBr <= a.vmin;  // wave-uniform
     u32x4 d[CPT][K];
     gf8_load<K, R, CPT, NT, CS, BUF>(a, obj, off, full, d);
     u32x4 acc[CPT][R];
@@ -1252,6 +1256,10 @@ inline void gf8_tables(uint32_t c, uint32_t t[5]) {
 int device_cus();  // compute units of the current device (kernels.hip)
 int gfp_blocks_per_cu();  // resident-grid size of gfp_apply (kernels.hip)
 int gf8_tile_map();       // gf8_apply workgroup -> tile order (kernels.hip)
+int gf8_wg_env();         // LEOEC_GF8_WG override of the tile width (kernels.hip)
+// Blocks larger than this run gf8_apply with 64-lane workgroups: 1 MiB objects
+// (bs 104,960) keep 256 lanes, 2 MiB (209,792) and up take 64.
+constexpr uint64_t kGf8NarrowBytes = 160 * 1024;
 
 // BRANCHY = -1: pick per launch from the coefficients (scalar-branch form
 // when enough coefficients are 0/1, the paired all-table form otherwise).
@@ -1279,7 +1287,15 @@ int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
       n01 += cf <= 1;
     }
   }
-  const uint32_t tb = (uint32_t)WG * 16u * CPT;
+  // Workgroup (= tile) width: WG lanes, or 64 lanes (1 KiB tiles) for blocks
+  // above kGf8NarrowBytes, where they measured 2-8 % faster (block
+  // size sweep); LEOEC_GF8_WG=64|256 forces one (A/B, parity tests).
+  uint32_t wg = (uint32_t)WG;
+  if (CPT == 1 && !PIPE) {
+    const int force = gf8_wg_env();
+    if (force == 64 || (force == 0 && p.block_size > kGf8NarrowBytes)) wg = 64;
+  }
+  const uint32_t tb = wg * 16u * CPT;
   a.tiles = (uint32_t)((p.block_size + tb - 1) / tb);
   a.vmin = vmin;
   a.total_tiles = (uint32_t)(c.no * a.tiles);
@@ -1303,10 +1319,10 @@ int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   }
   if (branchy)
     hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, true, COPY, PIPE, LDS, WAVES, WG, XMAP, BUF>),
-                       dim3(grid), dim3(WG), 0, s, a);
+                       dim3(grid), dim3(wg), 0, s, a);
   else
     hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, false, COPY, PIPE, LDS, WAVES, WG, XMAP, BUF>),
-                       dim3(grid), dim3(WG), 0, s, a);
+                       dim3(grid), dim3(wg), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }
 

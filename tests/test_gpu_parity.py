@@ -338,6 +338,25 @@ def test_liberation_device_batch_forms(gpu, le, oracle, monkeypatch):
         assert outs[0][o].tobytes() == b"".join(ref[k:]), f"object {o}"
 
 
+@pytest.mark.parametrize("wg", ["64", "256"])
+def test_gf8_tile_width_forms(gpu, le, oracle, wg, monkeypatch):
+    """gf8_apply at both tile widths (64-lane workgroups are shipped for blocks
+    above 160 KiB, 256-lane below; LEOEC_GF8_WG forces one): sizes either side
+    of the switch, encode against the oracle, a 4-data-erasure decode round
+    trip and a data+parity repair."""
+    monkeypatch.setenv("LEOEC_GF8_WG", wg)
+    for cls, k, m in [("vandrs", 10, 4), ("isars", 10, 4), ("vandrs", 4, 2), ("vandrs", 17, 5)]:
+        for size in (1, 5000, 1048576, 2097152 + 12345):
+            data = rand_bytes(size, size + k)
+            st, blocks = le.nif_encode(cls, (k, m, 8), data, size)
+            assert st == "ok" and blocks == oracle.encode(cls, k, m, 8, data), (cls, k, m, size)
+            ids = list(range(m, k + m))
+            st, out = le.nif_decode(cls, (k, m, 8), [blocks[i] for i in ids], ids, size)
+            assert st == "ok" and out == data, (cls, k, m, size)
+            st, rep = le.nif_repair(cls, (k, m, 8), [blocks[i] for i in ids], ids, [0, k])
+            assert st == "ok" and rep == [blocks[0], blocks[k]], (cls, k, m, size)
+
+
 def test_golden_fixtures_gpu(gpu, le):
     """The committed restatement-derived fixtures, through the GPU engine."""
     import json

@@ -13,7 +13,7 @@
 // Cache policy = gfx950 buffer aux bits (1 sc0, 2 nt, 16 sc1).
 //
 //   hipcc --offload-arch=gfx950 -O3 -o tools/stream_ceiling tools/stream_ceiling.hip
-//   tools/stream_ceiling [reps] [const|random]
+//   tools/stream_ceiling [reps] [const|random] [object bytes]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,8 +33,13 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   } while (0)
 
 constexpr int K = 10, R = 4;
-constexpr unsigned BS = 104960, OBJ = 1u << 20, TILE = 4096, TILES = (BS + TILE - 1) / TILE;
-constexpr unsigned NOBJ = 1024;
+// Geometry (argv[3] = object bytes, default 1 MiB: bs = 104,960, 1024 objects;
+// 64 MiB: bs = 6,710,912, 16 objects — BASELINE cfg4).
+struct Geo {
+  unsigned bs;
+  unsigned long long obj;  // object stride
+  unsigned nobj;
+};
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
@@ -42,9 +47,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
 
 template <int MODE, int LA, int SA, int CPT = 1, int SEQ = 1, int WG = 256>
 __global__ void __launch_bounds__(WG) pattern(const unsigned char* __restrict__ in,
-                                              unsigned char* __restrict__ out, int flag) {
+                                              unsigned char* __restrict__ out, int flag, Geo geo) {
+  const unsigned BS = geo.bs, NOBJ = geo.nobj;
+  const unsigned long long OBJ = geo.obj;
   constexpr unsigned TB = WG * 16u * CPT;                 // bytes of a block per tile
-  constexpr unsigned NT = (BS + TB - 1) / TB;            // tiles per block
+  const unsigned NT = (BS + TB - 1) / TB;                // tiles per block
   for (int q = 0; q < SEQ; ++q) {
     const unsigned g = blockIdx.x * SEQ + q;
     if (g >= NOBJ * NT) return;
@@ -111,25 +118,35 @@ __global__ void fill_random(unsigned* p, size_t n, unsigned seed) {  // splitmix
 
 struct Case {
   const char* name;
-  void (*k)(const unsigned char*, unsigned char*, int);
+  void (*k)(const unsigned char*, unsigned char*, int, Geo);
   double bytes;  // algorithmic bytes per launch
   unsigned grid, wg;
 };
 
-#define PATX(M, L, S, C, Q, W) reinterpret_cast<void (*)(const unsigned char*, unsigned char*, int)>(&pattern<M, L, S, C, Q, W>)
+#define PATX(M, L, S, C, Q, W) reinterpret_cast<void (*)(const unsigned char*, unsigned char*, int, Geo)>(&pattern<M, L, S, C, Q, W>)
 #define PAT(M, L, S) PATX(M, L, S, 1, 1, 256)
-constexpr unsigned grid_of(unsigned cpt, unsigned seq, unsigned wg) {
-  return (NOBJ * ((BS + wg * 16u * cpt - 1) / (wg * 16u * cpt)) + seq - 1) / seq;
+static Geo G;
+unsigned grid_of(unsigned cpt, unsigned seq, unsigned wg) {
+  return (G.nobj * ((G.bs + wg * 16u * cpt - 1) / (wg * 16u * cpt)) + seq - 1) / seq;
 }
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 50;
+  const unsigned long long osz = argc > 3 ? strtoull(argv[3], nullptr, 10) : (1ull << 20);
+  // leo_erasure geometry (c_src/common.cpp:24-33, rscoding.cpp:44), w = 8:
+  // bs = ceil16(ceil(N / (k w))) * w  (a multiple of 128: whole cache lines)
+  G.bs = (unsigned)(((osz + 8 * K - 1) / (8 * K) + 15) / 16 * 16 * 8);
+  G.obj = osz;
+  G.nobj = (unsigned)((1ull << 30) / osz);
+  const unsigned BS = G.bs, NOBJ = G.nobj;
+  const unsigned long long OBJ = G.obj;
+  printf("# object %llu B, bs %u, %u objects\n", OBJ, BS, NOBJ);
   unsigned char *in, *out;
   const double rd = (double)NOBJ * K * BS, wr = (double)NOBJ * R * BS;
   const size_t ncopy = (size_t)((rd + wr) / 2 / 16);  // flat copy: same bytes moved as the pattern
   // both buffers hold the pattern's footprint and the flat copy's (the copy
   // moves (rd + wr) / 2 bytes each way, more than the parity buffer)
-  const size_t in_bytes = std::max((size_t)NOBJ * OBJ + (1 << 20), ncopy * 16);
+  const size_t in_bytes = std::max((size_t)(NOBJ * OBJ + (size_t)K * BS), ncopy * 16);
   const size_t out_bytes = std::max((size_t)NOBJ * R * BS, ncopy * 16);
   CHECK(hipMalloc(&in, in_bytes));
   CHECK(hipMalloc(&out, out_bytes));
@@ -167,7 +184,7 @@ int main(int argc, char** argv) {
     for (size_t c = 0; c < cases.size() + 2; ++c) {
       auto launch = [&]() {
         if (c < cases.size())
-          hipLaunchKernelGGL(cases[c].k, dim3(cases[c].grid), dim3(cases[c].wg), 0, 0, in, out, 0);
+          hipLaunchKernelGGL(cases[c].k, dim3(cases[c].grid), dim3(cases[c].wg), 0, 0, in, out, 0, G);
         else if (c == cases.size())
           hipLaunchKernelGGL((flat_copy<2, 2>), dim3((unsigned)((ncopy + 255) / 256)), dim3(256), 0, 0,
                              (const u32x4*)in, (u32x4*)out, ncopy);
