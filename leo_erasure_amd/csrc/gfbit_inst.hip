@@ -82,8 +82,21 @@ int prefetch_env() {
   return e ? std::atoi(e) : kPF;
 }
 
+// LEOEC_GFBIT_WG=64 (measurement): 64-lane workgroups (512-B tiles per packet)
+template <int W, int LW>
+GfbFn pick_r_wg64(int r, bool acc) {
+  static const GfbFn tbl[2][kMaxR] = {
+      {&launch_gfb_t<W, 1, LW, false, kPF, false, 0, 64>, &launch_gfb_t<W, 2, LW, false, kPF, false, 0, 64>,
+       &launch_gfb_t<W, 3, LW, false, kPF, false, 0, 64>, &launch_gfb_t<W, 4, LW, false, kPF, false, 0, 64>},
+      {&launch_gfb_t<W, 1, LW, true, kPF, false, 0, 64>, &launch_gfb_t<W, 2, LW, true, kPF, false, 0, 64>,
+       &launch_gfb_t<W, 3, LW, true, kPF, false, 0, 64>, &launch_gfb_t<W, 4, LW, true, kPF, false, 0, 64>}};
+  return tbl[acc ? 1 : 0][r - 1];
+}
+
 GfbFn pick(int w, int r, bool acc, int nk) {
   if (w == 8) {
+    if (const char* wg = std::getenv("LEOEC_GFBIT_WG"))
+      if (std::atoi(wg) == 64) return pick_r_wg64<8, 2>(r, acc);
     const int lw = lane_width_env();
     const char* ce = std::getenv("LEOEC_GFBIT_CEIL");  // measurement only: not a code
     if (ce && std::atoi(ce) && r == 4 && !acc) return &launch_gfb_t<8, 4, 2, false, kPF, true>;
