@@ -133,6 +133,12 @@ def main():
                 "isars(10,4,8) 1 MiB x1024")
     stripe_case(torch, le, "liberation", 7, 2, 7, MiB, 1024, R, [0, 1], None,
                 "liberation(7,2,7) 1 MiB x1024")
+    stripe_case(torch, le, "liberation", 4, 2, 7, MiB, 1024, R, [0, 1], None,
+                "liberation(4,2,7) 1 MiB x1024")
+    stripe_case(torch, le, "liberation", 10, 2, 11, MiB, 1024, R, [0, 1], None,
+                "liberation(10,2,11) 1 MiB x1024")
+    stripe_case(torch, le, "vandrs", 10, 4, 8, 16 * MiB, 64, R, [0, 1, 2, 3], None,
+                "vandrs RS(10,4,8) 16 MiB x64")
     stripe_case(torch, le, "vandrs", 10, 4, 16, MiB, 512, R, [0, 1, 2, 3], None,
                 "vandrs RS(10,4,16) 1 MiB x512")
     stripe_case(torch, le, "vandrs", 10, 4, 32, MiB, 256, R, [0, 1, 2, 3], None,
