@@ -193,6 +193,62 @@ int bit_rows(const Code& c, const int* surv, const int* want, int nwant,
   return LEOEC_OK;
 }
 
+// Liberation decode / repair of erased data blocks as syndromes + a small
+// inverse (kernels_impl.hpp lib_dec_apply).  Applies when every wanted block
+// is an erased data block (not in the survivor set); LEOEC_E_UNSUPPORTED
+// sends the caller to the generic bitmatrix path (wanted coding blocks,
+// encode).  E = data ids missing from S, C = coding ids in S, |C| = |E|;
+// the map is rows(wanted) of (B_CE)^-1 applied to S_C = B_CS' D_S' ^ C.
+int lib_dec_plan(const Code& c, const int* surv, const std::vector<Shard>& in, const int* want,
+                 const std::vector<Shard>& out, LibDecApply* p) {
+  const int k = c.k, w = c.w, nwant = (int)out.size();
+  if (c.m != 2 || nwant < 1 || nwant > 2) return LEOEC_E_UNSUPPORTED;
+  std::vector<int> pos(k + 2, -1);  // id -> index in `in`
+  for (int i = 0; i < k; ++i) {
+    if (surv[i] < 0 || surv[i] >= k + 2) return LEOEC_E_ARG;
+    pos[surv[i]] = i;
+  }
+  std::vector<int> E, C;
+  for (int j = 0; j < k; ++j)
+    if (pos[j] < 0) E.push_back(j);
+  for (int r = 0; r < 2; ++r)
+    if (pos[k + r] >= 0) C.push_back(r);
+  if (E.empty() || E.size() != C.size()) return LEOEC_E_UNSUPPORTED;
+  std::vector<int> wi(nwant);  // wanted block -> index in E
+  for (int b = 0; b < nwant; ++b) {
+    const auto it = std::find(E.begin(), E.end(), want[b]);
+    if (it == E.end()) return LEOEC_E_UNSUPPORTED;
+    wi[b] = (int)(it - E.begin());
+  }
+  const int e = (int)E.size(), n = e * w;
+  BitMatrix A, inv;  // A = B_CE: rows of C's coding blocks, columns of E's data blocks
+  A.resize(n, n);
+  for (int ic = 0; ic < e; ++ic)
+    for (int r = 0; r < w; ++r)
+      for (int ie = 0; ie < e; ++ie)
+        for (int x = 0; x < w; ++x)
+          if (c.B.get(C[ic] * w + r, E[ie] * w + x)) A.set(ic * w + r, ie * w + x, true);
+  const int rc = bit_invert(A, &inv);
+  if (rc) return rc;
+  p->w = w;
+  p->k = k;
+  p->data.assign(k, Shard{nullptr, 0, 0});
+  for (int j = 0; j < k; ++j)
+    if (pos[j] >= 0) p->data[j] = in[pos[j]];
+  p->cod.assign(2, Shard{nullptr, 0, 0});
+  for (int r = 0; r < 2; ++r)
+    if (pos[k + r] >= 0) p->cod[r] = in[pos[k + r]];
+  p->out = out;
+  p->mbits.assign((size_t)nwant * 2 * w, 0u);
+  for (int b = 0; b < nwant; ++b)
+    for (int x = 0; x < w; ++x)
+      for (int ic = 0; ic < e; ++ic)
+        for (int r = 0; r < w; ++r)
+          if (inv.get(wi[b] * w + x, ic * w + r))
+            p->mbits[(size_t)b * 2 * w + C[ic] * w + r] |= 1u << (31 - x);
+  return LEOEC_OK;
+}
+
 namespace {
 // LEOEC_BITMATRIX=1 forces the generic masked-bitmatrix kernel for cauchyrs
 // (measurement / cross-check of the bitsliced GF path).
@@ -233,6 +289,16 @@ int apply(const Code& c, const int* surv, const std::vector<Shard>& in, const in
     p.block_size = bs;
     p.nobj = nobj;
     return launch(p, s);
+  }
+  if (c.coding == LEOEC_LIBERATION && lib_dec_supported(c.w)) {
+    LibDecApply p;
+    const int rc = lib_dec_plan(c, surv, in, want, out, &p);
+    if (rc == LEOEC_OK) {
+      p.block_size = bs;
+      p.nobj = nobj;
+      return launch(p, s);
+    }
+    if (rc != LEOEC_E_UNSUPPORTED) return rc;  // else: the generic bitmatrix path
   }
   BitApply p;
   p.w = c.w;

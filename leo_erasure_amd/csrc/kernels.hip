@@ -254,6 +254,67 @@ int launch(const GfApply& p, hipStream_t s) {
   return LEOEC_OK;
 }
 
+namespace {
+using LibDecFn = void (*)(const detail::LibDecArgs);
+LibDecFn lib_dec_kernel(int w) {
+  switch (w) {
+    case 3: return &detail::lib_dec_apply<3>;
+    case 5: return &detail::lib_dec_apply<5>;
+    case 7: return &detail::lib_dec_apply<7>;
+    case 11: return &detail::lib_dec_apply<11>;
+    case 13: return &detail::lib_dec_apply<13>;
+    default: return nullptr;
+  }
+}
+}  // namespace
+
+bool lib_dec_supported(int w) {
+  return env_int("LEOEC_LIB_FORM", 1) != 0 && lib_dec_kernel(w) != nullptr;
+}
+
+int launch(const LibDecApply& p, hipStream_t s) {
+  const int w = p.w;
+  const LibDecFn fn = lib_dec_kernel(w);
+  const int nout = (int)p.out.size();
+  if (!fn || p.k <= 0 || p.k > w || (int)p.data.size() != p.k || p.cod.size() != 2 || nout < 1 ||
+      nout > 2 || p.mbits.size() != (size_t)nout * 2 * w)
+    return LEOEC_E_ARG;
+  if (p.block_size == 0 || p.nobj == 0) return LEOEC_OK;
+  if (p.block_size % ((uint64_t)16 * w) || p.block_size >= (1ull << 32)) return LEOEC_E_BAD_SIZE;
+  for (const auto* v : {&p.data, &p.cod, &p.out})
+    for (const Shard& sh : *v)
+      if (sh.base && (((uintptr_t)sh.base & 15u) || (sh.stride & 15u))) return LEOEC_E_ARG;
+  const uint32_t ps = (uint32_t)(p.block_size / (uint64_t)w);
+  const uint32_t tiles = (ps + kTileBytes - 1) / kTileBytes;
+  const uint64_t max_obj = (uint64_t)0x7FFFFFFF / tiles;
+  for (uint64_t o0 = 0; o0 < p.nobj; o0 += max_obj) {
+    const uint64_t no = (p.nobj - o0 < max_obj) ? p.nobj - o0 : max_obj;
+    LibDecArgs a;
+    a.k = p.k;
+    a.nout = nout;
+    a.ps = ps;
+    a.tiles = tiles;
+    uint32_t vmin = 0xFFFFFFFFu;
+    auto take = [&](const Shard& sh) {
+      if (!sh.base) return DevShard{nullptr, 0, 0, 0};
+      const DevShard d = dev_shard(sh, o0);
+      if (d.valid < vmin) vmin = d.valid;
+      return d;
+    };
+    for (int j = 0; j < kMaxK; ++j) a.data[j] = j < p.k ? take(p.data[j]) : DevShard{nullptr, 0, 0, 0};
+    for (int r = 0; r < 2; ++r) a.cod[r] = take(p.cod[r]);
+    for (int b = 0; b < 2; ++b) {
+      a.out[b] = b < nout ? take(p.out[b]) : DevShard{nullptr, 0, 0, 0};
+      for (int q = 0; q < 32; ++q)
+        a.mbits[b][q] = (b < nout && q < 2 * w) ? p.mbits[(size_t)b * 2 * w + q] : 0u;
+    }
+    a.vmin = vmin;
+    hipLaunchKernelGGL(fn, dim3((uint32_t)(no * tiles)), dim3(kThreads), 0, s, a);
+    if (hipGetLastError() != hipSuccess) return LEOEC_E_HIP;
+  }
+  return LEOEC_OK;
+}
+
 int launch(const BitApply& p, hipStream_t s) {
   const int w = p.w;
   if (w <= 0 || w > 32 || p.KB <= 0 || p.RB <= 0 || (int)p.in.size() != p.KB ||

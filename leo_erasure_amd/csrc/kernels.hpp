@@ -60,10 +60,25 @@ struct GfBitApply {
   uint64_t nobj = 0;
 };
 
+// Liberation decode / repair of erased data blocks through syndromes
+// (kernels_impl.hpp lib_dec_apply): data[j] = surviving data block j (base
+// nullptr if erased), cod[0..1] = P, Q if survivors; the wanted outputs are
+// erased data blocks; mbits[b][s] holds, for wanted block b and syndrome
+// packet s (P 0..w-1, Q w..2w-1), bit 31-x set when s feeds packet x.
+struct LibDecApply {
+  int w = 0, k = 0;
+  std::vector<Shard> data, cod, out;  // k, 2, nout (<= 2) shards
+  std::vector<uint32_t> mbits;        // nout x 2w
+  uint64_t block_size = 0;
+  uint64_t nobj = 0;
+};
+
 // Enqueue on `stream`; returns a leoec_status.
 int launch(const GfApply& plan, hipStream_t stream);
 int launch(const BitApply& plan, hipStream_t stream);
 int launch(const GfBitApply& plan, hipStream_t stream);
+int launch(const LibDecApply& plan, hipStream_t stream);
 bool gfbit_supported(int w);
+bool lib_dec_supported(int w);  // a lib_dec_apply instance exists and LEOEC_LIB_FORM != 0
 
 }  // namespace leoec

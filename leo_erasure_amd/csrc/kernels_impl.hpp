@@ -890,6 +890,118 @@ lib_apply(const LibArgs a) {
 }
 
 // ===========================================================================
+// Liberation decode / data repair through syndromes.  The decoding
+// bitmatrix G_S^-1 of the survivor set S is ~45 % ones (an inverse), so the
+// masked kernel pays 2w v_bitop3 per input packet dword and is VALU-bound at
+// w >= 11.  Instead, with E the erased data blocks and C the coding blocks
+// in S (|C| = |E| <= 2):
+//   syndrome  S_c = c ^ sum over surviving data j of B_cj D_j   (c in C)
+//             (the liberation encode structure of lib_apply, static)
+//   data      D_E = (B_CE)^-1 S_C                                (eW x eW)
+// B_CE^-1 is built on the host; its rows for the wanted blocks come as one
+// mask word per syndrome packet.  For every input the result is the one
+// linear map G_S^-1 restricted to the wanted rows (the survivors determine
+// the codeword uniquely), so outputs equal the generic path's bit for bit.
+struct LibDecArgs {
+  DevShard data[kMaxK];   // data block j (base nullptr if erased)
+  DevShard cod[2];        // P, Q (base nullptr if not a survivor)
+  DevShard out[2];        // wanted (erased data) blocks
+  uint32_t mbits[2][32];  // [wanted block][syndrome packet s: P 0..W-1, Q W..2W-1]:
+                          // bit (31 - x) set => feeds output packet x
+  int k;
+  int nout;
+  uint32_t ps;
+  uint32_t tiles;
+  uint32_t vmin;          // min valid over every shard read or written
+};
+
+constexpr int lib_dec_waves(int w) { return w <= 5 ? 4 : w <= 11 ? 3 : 2; }
+
+template <int W>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(lib_dec_waves(W), 8)))
+lib_dec_apply(const LibDecArgs a) {
+  const uint32_t obj = blockIdx.x / a.tiles;
+  const uint32_t tile = blockIdx.x - obj * a.tiles;
+  const uint32_t t0 = tile * kTileBytes;
+  const uint32_t off = t0 + threadIdx.x * 16u;
+  if (off >= a.ps) return;
+  const uint64_t o64 = obj;
+  const bool full = t0 + kTileBytes <= a.ps &&
+                    (uint64_t)(W - 1) * a.ps + t0 + kTileBytes <= (uint64_t)a.vmin;
+  auto load = [&](const DevShard& sh, int x) {
+    const uint8_t* b = sh.base + o64 * sh.stride;
+    const uint32_t pk = (uint32_t)x * a.ps;
+    if (full) return ld16<true>(b + pk + off);
+    const uint32_t v = sh.valid;
+    return load_guarded(b + pk, off, v > pk ? v - pk : 0u);
+  };
+  // One static packet stream: P (W packets), Q (W), then data blocks 0..k-1,
+  // with the loads of the next LA packets in flight (as lib_apply).  Absent
+  // shards (P or Q not a survivor, erased data blocks) read as zero without
+  // a memory access, so the stream's register indices stay static.
+  constexpr int LA = 2, RS = LA + 1, NP = (W + 2) * W;
+  auto shard_of = [&](int blk) -> const DevShard& {  // blk: 0 P, 1 Q, 2 + j data j
+    return blk < 2 ? a.cod[blk] : a.data[blk - 2];
+  };
+  auto fetch = [&](int q) {
+    const int blk = q / W;
+    const DevShard& sh = shard_of(blk);
+    if ((blk >= 2 && blk - 2 >= a.k) || sh.base == nullptr) return u32x4{0u, 0u, 0u, 0u};
+    return load(sh, q % W);
+  };
+  u32x4 S[2 * W];  // P syndromes, then Q syndromes
+#pragma unroll
+  for (int s = 0; s < 2 * W; ++s) S[s] = u32x4{0u, 0u, 0u, 0u};
+  u32x4 ring[RS];
+#pragma unroll
+  for (int q = 0; q < LA; ++q) ring[q] = fetch(q);
+#pragma unroll
+  for (int blk = 0; blk < W + 2; ++blk) {
+    if (blk >= 2 && blk - 2 >= a.k) break;
+    const int j = blk - 2;
+    const int y = j > 0 ? (j * ((W - 1) / 2)) % W : 0;
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const int p = blk * W + x, q = p + LA;
+      if (q < NP) ring[q % RS] = fetch(q);
+      const u32x4 v = ring[p % RS];
+      if (blk < 2) {
+        S[blk * W + x] ^= v;
+      } else {
+        S[x] ^= v;
+        S[W + (x - j + W) % W] ^= v;
+        if (j > 0 && x == (y + j - 1) % W) S[W + y] ^= v;
+      }
+    }
+  }
+  for (int b = 0; b < a.nout; ++b) {
+    u32x4 acc[W];
+#pragma unroll
+    for (int x = 0; x < W; ++x) acc[x] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int s = 0; s < 2 * W; ++s) {
+      const uint32_t bits = a.mbits[b][s];  // wave-uniform
+      if (bits != 0u) {
+#pragma unroll
+        for (int x = 0; x < W; ++x) {
+          const uint32_t m = (uint32_t)((int32_t)(bits << x) >> 31);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[x][e] ^= S[s][e] & m;
+        }
+      }
+    }
+    uint8_t* ob = const_cast<uint8_t*>(a.out[b].base) + o64 * a.out[b].stride;
+    const uint32_t v = a.out[b].valid;
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const uint32_t pk = (uint32_t)x * a.ps;
+      if (full) st16<true>(ob + pk + off, acc[x]);
+      else store_guarded(ob + pk, off, v > pk ? v - pk : 0u, acc[x]);
+    }
+  }
+}
+
+// ===========================================================================
 // GF(2^w) on packet-bitsliced blocks (cauchyrs).  Each lane owns LW dwords of
 // every packet.  Per input block: y = its w packets; for t = 0..w-1, every
 // output block whose coefficient has bit t set gets y xor-ed in, then

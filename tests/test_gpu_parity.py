@@ -316,6 +316,16 @@ def test_liberation_encode_forms(gpu, le, oracle, form, monkeypatch):
             assert st == "ok" and out == data, (k, w)
             st, rep = le.nif_repair("liberation", (k, 2, w), [blocks[i] for i in ids], ids, [0, k, k + 1])
             assert st == "ok" and rep == [blocks[0], blocks[k], blocks[k + 1]], (k, w)
+            # syndrome decode (lib_dec_apply) shapes: one data block lost with P
+            # (solved through Q alone), and one of two lost data blocks wanted
+            lost = [k - 1, k]
+            ids = [i for i in range(k + 2) if i not in lost]
+            st, out = le.nif_decode("liberation", (k, 2, w), [blocks[i] for i in ids], ids, size)
+            assert st == "ok" and out == data, (k, w, lost)
+            if k >= 2:
+                ids = list(range(2, k + 2))
+                st, rep = le.nif_repair("liberation", (k, 2, w), [blocks[i] for i in ids], ids, [1])
+                assert st == "ok" and rep == [blocks[1]], (k, w)
 
 
 def test_liberation_device_batch_forms(gpu, le, oracle, monkeypatch):
