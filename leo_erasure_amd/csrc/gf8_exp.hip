@@ -31,6 +31,7 @@ ChunkFn gf8_variant(int v) {
     case 30: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 256, false, true>;  // buffer ld/st
     case 31: return &launch_gf8_t<10, 4, false, 1, true, 1, true, false, false, 5, 256, false, true>;  // copy buffer
     case 32: return &launch_gf8_t<10, 4, false, 1, true, -1, false, false, true, 5, 256, false, true>; // buffer, auto branchy
+    case 33: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 256, false, false, true>;  // row 0 / column 0 of ones folded
     case 29: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 6, 64>;   // wg64 >=6 waves
     default: return nullptr;
   }

@@ -231,6 +231,76 @@ __device__ __forceinline__ void gf8_tile(const Gf8Args<K, R>& a, const Gf8Lds<K,
   }
 }
 
+// As gf8_tile (paired form) for a matrix whose row 0 and column 0 are all
+// ones (every vandrs encode matrix): those K+R-1
+// coefficients contribute the data word itself (one term) instead of three
+// table lookups; every term of a row is folded pairwise into xor3 with the
+// pairing worked out at compile time.  The launcher checks the property.
+template <int K, int R, int CPT, bool LDS>
+__device__ __forceinline__ void gf8_tile_ones(const Gf8Lds<K, R>& lds, const u32x4 (&d)[CPT][K],
+                                              u32x4 (&acc)[CPT][R]) {
+  u32x4 pend[CPT][R];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    uint32_t s0[CPT][4], s1[CPT][4], s2[CPT][4];
+    if (j > 0) {
+#pragma unroll
+      for (int c = 0; c < CPT; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t x = d[c][j][e];
+          s0[c][e] = x & 0x07070707u;
+          s1[c][e] = (x >> 3) & 0x07070707u;
+          s2[c][e] = (x >> 6) & 0x03030303u;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool one = r == 0 || j == 0;
+      int pos = 0;  // terms of row r before coefficient j (folds to a constant)
+#pragma unroll
+      for (int jj = 0; jj < j; ++jj) pos += (r == 0 || jj == 0) ? 1 : 3;
+      uint32_t t0l = 0, t0h = 0, t1l = 0, t1h = 0, t2 = 0;
+      if (!one) {
+        const u32x4 t = lds.t[r * K + j][0];
+        t0l = t[0]; t0h = t[1]; t1l = t[2]; t1h = t[3];
+        t2 = lds.t[r * K + j][1][0];
+      }
+#pragma unroll
+      for (int c = 0; c < CPT; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          uint32_t term[3];
+          int n = 1;
+          if (one) {
+            term[0] = d[c][j][e];
+          } else {
+            term[0] = perm(t0h, t0l, s0[c][e]);
+            term[1] = perm(t1h, t1l, s1[c][e]);
+            term[2] = perm(t2, t2, s2[c][e]);
+            n = 3;
+          }
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            if (i >= n) break;
+            if (((pos + i) & 1) == 0) pend[c][r][e] = term[i];
+            else acc[c][r][e] = xor3(acc[c][r][e], pend[c][r][e], term[i]);
+          }
+        }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    int tot = 0;
+#pragma unroll
+    for (int jj = 0; jj < K; ++jj) tot += (r == 0 || jj == 0) ? 1 : 3;
+    if (tot & 1) {
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) acc[c][r] ^= pend[c][r];
+    }
+  }
+}
+
 template <int K, int R, int CPT, bool NT, uint32_t CS = kTileBytes, bool BUF = false>
 __device__ __forceinline__ void gf8_load(const Gf8Args<K, R>& a, uint64_t o, uint32_t off,
                                          bool full, u32x4 (&d)[CPT][K]) {
@@ -318,7 +388,7 @@ __device__ __forceinline__ uint32_t xcd_group(uint32_t b, uint32_t n) {
 // that walks the tiles and issues the loads of its next tile before
 // computing the current one (PIPE = true).
 template <int K, int R, bool ACC, int CPT, bool NT, bool BRANCHY, bool COPY, bool PIPE, bool LDS,
-          int WAVES, int WG, bool XMAP, bool BUF = false>
+          int WAVES, int WG, bool XMAP, bool BUF = false, bool ONES = false>
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 gf8_apply(const Gf8Args<K, R> a) {
   constexpr uint32_t CS = (uint32_t)WG * 16u;  // bytes of one column group
@@ -354,7 +424,10 @@ gf8_apply(const Gf8Args<K, R> a) {
     gf8_load<K, R, CPT, NT, CS, BUF>(a, obj, off, full, d);
     u32x4 acc[CPT][R];
     gf8_init_store<K, R, ACC, CPT, NT, CS>(a, obj, off, acc);
-    gf8_tile<K, R, CPT, BRANCHY, COPY, LDS>(a, lds, d, acc);
+    if (ONES && LDS && !COPY)
+      gf8_tile_ones<K, R, CPT, LDS>(lds, d, acc);
+    else
+      gf8_tile<K, R, CPT, BRANCHY, COPY, LDS>(a, lds, d, acc);
     gf8_store<K, R, CPT, NT, CS, BUF>(a, obj, off, full, acc);
     return;
   }
@@ -1378,7 +1451,7 @@ constexpr uint64_t kGf8NarrowBytes = 160 * 1024;
 template <int K, int R, bool ACC, int CPT = kGf8Default.cpt, bool NT = kGf8Default.nt,
           int BRANCHY = kGf8Default.branchy, bool COPY = kGf8Default.copy, bool PIPE = false,
           bool LDS = kGf8Default.lds, int WAVES = kGf8Default.waves, int WG = kThreads,
-          bool XMAP = false, bool BUF = false>
+          bool XMAP = false, bool BUF = false, bool ONES = false>
 int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   Gf8Args<K, R> a;
   a.one = a.zero = 0;
@@ -1428,6 +1501,16 @@ int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   if (PIPE) {
     const uint32_t cap = (uint32_t)device_cus() * 4u;
     grid = grid < cap ? grid : cap;
+  }
+  // ONES: row 0 and column 0 of this launch's coefficients are all 1
+  bool ones = ONES && c.r0 == 0 && c.j0 == 0;
+  for (int r = 0; ones && r < R; ++r)
+    for (int j = 0; ones && j < K; ++j)
+      if ((r == 0 || j == 0) && (p.coef[(size_t)r * p.K + j] & 0xFFu) != 1u) ones = false;
+  if (ONES && ones) {
+    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, false, COPY, PIPE, LDS, WAVES, WG, XMAP, BUF, true>),
+                       dim3(grid), dim3(wg), 0, s, a);
+    return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
   }
   if (branchy)
     hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, true, COPY, PIPE, LDS, WAVES, WG, XMAP, BUF>),
