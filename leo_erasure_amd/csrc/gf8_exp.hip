@@ -20,18 +20,19 @@ ChunkFn gf8_variant(int v) {
     case 16: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 6>;  // >=6 waves
     case 17: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 8>;  // 8 waves
     case 20: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 512>;
-    case 21: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 256, true>;
-    case 22: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 512, true>;
+    case 21: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 256, 1>;
+    case 22: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 512, 1>;
     case 23: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 1024>;
-    case 24: return &launch_gf8_t<10, 4, false, 1, true, 1, true, false, false, 5, 256, true>;  // copy xmap
+    case 24: return &launch_gf8_t<10, 4, false, 1, true, 1, true, false, false, 5, 256, 1>;  // copy xmap
     case 25: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 64>;   // wg64
     case 26: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 128>;  // wg128
     case 27: return &launch_gf8_t<10, 4, false, 1, true, 1, true, false, false, 5, 64>;   // copy wg64
     case 28: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 4, 64>;   // wg64 >=4 waves
-    case 30: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 256, false, true>;  // buffer ld/st
-    case 31: return &launch_gf8_t<10, 4, false, 1, true, 1, true, false, false, 5, 256, false, true>;  // copy buffer
-    case 32: return &launch_gf8_t<10, 4, false, 1, true, -1, false, false, true, 5, 256, false, true>; // buffer, auto branchy
-    case 33: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 256, false, false, true>;  // row 0 / column 0 of ones folded
+    case 30: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 256, 2, true>;  // buffer ld/st
+    case 31: return &launch_gf8_t<10, 4, false, 1, true, 1, true, false, false, 5, 256, 2, true>;  // copy buffer
+    case 32: return &launch_gf8_t<10, 4, false, 1, true, -1, false, false, true, 5, 256, 2, true>; // buffer, auto branchy
+    case 33: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 256, 2, false, true>;  // row 0 / column 0 of ones folded
+    case 34: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 256, 2>;  // xcd_obj_map always
     case 29: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 6, 64>;   // wg64 >=6 waves
     default: return nullptr;
   }

@@ -16,7 +16,7 @@ using GfbFn = int (*)(const GfBitApply&, int r0, int j0, int nk, uint64_t o0, ui
                       hipStream_t);
 
 template <int W, int R, int LW, bool ACC, int PF, bool CEIL = false, int KR = 0,
-          int WG = kThreads, bool XMAP = false>
+          int WG = kThreads, int XMAP = 0>
 int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
                  hipStream_t s) {
   GfbArgs<R> a;
@@ -31,6 +31,10 @@ int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint6
     for (int j = 0; j < kMaxK; ++j)
       a.coef[i][j] = j < nk ? p.coef[(size_t)(r0 + i) * p.K + j0 + j] : 0u;
   }
+  // objects interleaved over the XCDs (xcd_obj_map) for objects of at most
+  // kObjMapMaxTiles tiles; LEOEC_GFBIT_XMAP=0 turns it off (A/B)
+  const char* xe = std::getenv("LEOEC_GFBIT_XMAP");
+  a.xmap = (XMAP == 0 && a.tiles <= kObjMapMaxTiles && !(xe && std::atoi(xe) == 0)) ? 1u : 0u;
   if (KR > 0 && nk > KR) return LEOEC_E_ARG;
   hipLaunchKernelGGL((gfbit_apply<W, R, LW, ACC, PF, CEIL, KR, WG, XMAP>),
                      dim3((uint32_t)(no * a.tiles)), dim3(WG), 0, s, a);
@@ -46,6 +50,7 @@ int launch_gfb_lds_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, u
   a.K = nk;
   a.ps = (uint32_t)(p.block_size / (uint64_t)W);
   a.tiles = (a.ps + kGfbLdsSlice - 1) / kGfbLdsSlice;
+  a.xmap = 0;
   for (int j = 0; j < kMaxK; ++j)
     a.in[j] = j < nk ? dev_shard(p.in[j0 + j], o0) : DevShard{nullptr, 0, 0, 0};
   for (int i = 0; i < R; ++i) {
@@ -100,9 +105,12 @@ GfbFn pick(int w, int r, bool acc, int nk) {
     const int lw = lane_width_env();
     const char* ce = std::getenv("LEOEC_GFBIT_CEIL");  // measurement only: not a code
     if (ce && std::atoi(ce) && r == 4 && !acc) return &launch_gfb_t<8, 4, 2, false, kPF, true>;
-    // LEOEC_GFBIT_XMAP=1 (measurement): all tiles of an object on one XCD
+    // LEOEC_GFBIT_XMAP (measurement): 0 = workgroup ids in dispatch order,
+    // 1 = all tiles of an object on one XCD, contiguous object ranges per XCD;
+    // default: objects interleaved over the XCDs (xcd_obj_map) when an
+    // object has at most kObjMapMaxTiles tiles (launch_gfb_t)
     if (const char* xm = std::getenv("LEOEC_GFBIT_XMAP"))
-      if (std::atoi(xm) && r == 4 && !acc) return &launch_gfb_t<8, 4, 2, false, kPF, false, 0, kThreads, true>;
+      if (std::atoi(xm) == 1 && r == 4 && !acc) return &launch_gfb_t<8, 4, 2, false, kPF, false, 0, kThreads, 1>;
     // LEOEC_GFBIT_LDS=1 (measurement): LDS-staged inputs
     if (const char* le = std::getenv("LEOEC_GFBIT_LDS")) {
       if (std::atoi(le) == 1) {

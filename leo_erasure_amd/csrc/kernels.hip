@@ -75,12 +75,13 @@ ChunkFn gfw_pick(int r, bool acc) {
 //   4/5/6 masked, 2/3/5 packets ahead (4 = shipped)
 //   7 as 4, with all tiles of an object on one XCD
 //   8 as 4, output packets padded to 8 / 16 / 32 (4 pads to even)
+//   9 as 4, objects interleaved over the XCDs (xcd_obj_map)
 // Measured on liberation(7,2,7): masked beats branchy (the scalar branches
 // cost more than the masked xors they save); look-ahead depth see DESIGN.md.
 int bit_form_env() {
   const char* e = std::getenv("LEOEC_BIT_FORM");
   const int f = e ? std::atoi(e) : 4;
-  return (f >= 0 && f <= 8) ? f : 4;
+  return (f >= 0 && f <= 9) ? f : 4;
 }
 
 using BitFn = void (*)(const detail::BitArgs);
@@ -94,7 +95,8 @@ BitFn bit_kernel_f(int form) {
     case 3: return &detail::bit_apply<RO, ACC, true, 1>;
     case 5: return &detail::bit_apply<RO, ACC, false, 3>;
     case 6: return &detail::bit_apply<RO, ACC, false, 5>;
-    case 7: return &detail::bit_apply<RO, ACC, false, 2, true>;
+    case 7: return &detail::bit_apply<RO, ACC, false, 2, 1>;
+    case 9: return &detail::bit_apply<RO, ACC, false, 2, 2>;
     default: return &detail::bit_apply<RO, ACC, false, 2>;
   }
 }
@@ -152,6 +154,12 @@ LibFn lib_kernel_w(int la) {
   if (la == 8) return &detail::lib_apply<W, 8>;
   return &detail::lib_apply<W, 2>;
 }
+// LEOEC_LIB_XMAP=0 (A/B): workgroup ids in dispatch order instead of the
+// object-interleaved XCD map (xcd_obj_map, kernels_impl.hpp) that the
+// launchers use for objects of at most kObjMapMaxTiles tiles
+bool obj_map(uint32_t tiles, const char* env) {
+  return tiles <= kObjMapMaxTiles && env_int(env, 2) != 0;
+}
 LibFn lib_kernel(int w) {
   const int la = env_int("LEOEC_LIB_LA", 2);
   switch (w) {
@@ -174,6 +182,7 @@ int launch_lib(const BitApply& p, LibFn fn, hipStream_t s) {
     a.k = p.KB;
     a.ps = ps;
     a.tiles = tiles;
+    a.xmap = obj_map(tiles, "LEOEC_LIB_XMAP") ? 1u : 0u;
     uint32_t vmin = 0xFFFFFFFFu;
     for (int j = 0; j < kMaxK; ++j) {
       a.in[j] = j < p.KB ? dev_shard(p.in[j], o0) : DevShard{nullptr, 0, 0, 0};
@@ -207,6 +216,7 @@ int gfp_blocks_per_cu() { return env_int("LEOEC_GFP_BPC", 64); }
 // LEOEC_GF8_TMAP: gf8_apply workgroup -> tile order (Gf8Args::tmap), A/B only.
 int gf8_tile_map() { return env_int("LEOEC_GF8_TMAP", 0); }
 int gf8_wg_env() { return env_int("LEOEC_GF8_WG", 0); }
+bool gf8_tile_map_set() { return std::getenv("LEOEC_GF8_TMAP") != nullptr; }
 }  // namespace detail
 
 int launch(const GfApply& p, hipStream_t s) {
@@ -294,6 +304,7 @@ int launch(const LibDecApply& p, hipStream_t s) {
     a.nout = nout;
     a.ps = ps;
     a.tiles = tiles;
+    a.xmap = obj_map(tiles, "LEOEC_LIB_XMAP") ? 1u : 0u;
     uint32_t vmin = 0xFFFFFFFFu;
     auto take = [&](const Shard& sh) {
       if (!sh.base) return DevShard{nullptr, 0, 0, 0};

@@ -367,6 +367,36 @@ def test_gf8_tile_width_forms(gpu, le, oracle, wg, monkeypatch):
             assert st == "ok" and rep == [blocks[0], blocks[k]], (cls, k, m, size)
 
 
+@pytest.mark.parametrize("cls,k,m,w", [("vandrs", 10, 4, 8), ("cauchyrs", 10, 4, 8),
+                                       ("liberation", 7, 2, 7)])
+def test_xcd_object_map_batches(gpu, le, oracle, monkeypatch, cls, k, m, w):
+    """The object-interleaved XCD map (objects of <= 64 tiles) on batches that
+    are not a multiple of 8 objects (the tail keeps dispatch order): parity
+    identical with the map off, equal to the oracle, and decode in place."""
+    n, size = 13, 1048576 - 333
+    bs, _ = le.layout(cls, (k, m, w), size)
+    host, objs = _batch(gpu, n, size, max(k, m) * bs, 31)
+    ref = objs.clone()
+    outs = []
+    for env in (None, "0"):
+        for var in ("LEOEC_GF8_TMAP", "LEOEC_GFBIT_XMAP", "LEOEC_LIB_XMAP"):
+            if env is None:
+                monkeypatch.delenv(var, raising=False)
+            else:
+                monkeypatch.setenv(var, env)
+        parity = gpu.zeros((n, max(k, m) * bs), dtype=gpu.uint8, device="cuda")
+        le.device.encode(cls, (k, m, w), objs, size, parity)
+        objs[:, :2 * bs] = 0
+        le.device.decode(cls, (k, m, w), objs, size, parity, [0, 1])
+        gpu.cuda.synchronize()
+        assert gpu.equal(objs, ref), env
+        outs.append(parity.cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    for o in (0, 7, 8, 12):
+        r = oracle.encode(cls, k, m, w, host[o, :size].tobytes())
+        assert outs[0][o, :m * bs].tobytes() == b"".join(r[k:]), f"object {o}"
+
+
 def test_golden_fixtures_gpu(gpu, le):
     """The committed restatement-derived fixtures, through the GPU engine."""
     import json

@@ -16,7 +16,7 @@ NAMES = {1: "shipped (lds+paired)", 2: "cpt2", 3: "branchy sgpr", 4: "branchy ld
          17: "waves 8 (spills)", 20: "wg512", 21: "xcd-map", 22: "wg512+xcd-map", 23: "wg1024",
          24: "copy-xor xcd-map", 25: "wg64", 26: "wg128", 27: "copy-xor wg64", 28: "wg64 waves>=4",
          29: "wg64 waves>=6", 30: "buffer ld/st", 31: "copy-xor buffer", 32: "buffer auto-branchy",
-         33: "ones row/col folded"}
+         33: "ones row/col folded", 34: "xcd obj-interleave always"}
 DEFAULT = [1, 7, 20, 21, 22, 23, 24]
 
 
