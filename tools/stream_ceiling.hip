@@ -19,6 +19,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <string>
 #include <vector>
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -39,7 +41,18 @@ struct Geo {
   unsigned bs;
   unsigned long long obj;  // object stride
   unsigned nobj;
+  unsigned omap;           // 1: the engine's xcd_obj_map (kernels_impl.hpp)
 };
+
+// Same remap as the engine: XCD x (ids dealt round-robin) takes objects
+// o = x mod 8, each object's tiles in order; ids past the last whole group
+// of 8 objects keep their place.
+__device__ __forceinline__ unsigned obj_map(unsigned b, unsigned n, unsigned tiles) {
+  const unsigned full = (n / tiles / 8u) * 8u * tiles;
+  if (b >= full) return b;
+  const unsigned x = b % 8u, i = b / 8u;
+  return ((i / tiles) * 8u + x) * tiles + i % tiles;
+}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
@@ -53,7 +66,7 @@ __global__ void __launch_bounds__(WG) pattern(const unsigned char* __restrict__ 
   constexpr unsigned TB = WG * 16u * CPT;                 // bytes of a block per tile
   const unsigned NT = (BS + TB - 1) / TB;                // tiles per block
   for (int q = 0; q < SEQ; ++q) {
-    const unsigned g = blockIdx.x * SEQ + q;
+    const unsigned g = (SEQ == 1 && geo.omap) ? obj_map(blockIdx.x, gridDim.x, NT) : blockIdx.x * SEQ + q;
     if (g >= NOBJ * NT) return;
     const unsigned obj = g / NT, tile = g % NT;
     const unsigned char* ib = in + (size_t)obj * OBJ;
@@ -121,6 +134,7 @@ struct Case {
   void (*k)(const unsigned char*, unsigned char*, int, Geo);
   double bytes;  // algorithmic bytes per launch
   unsigned grid, wg;
+  unsigned omap = 0;
 };
 
 #define PATX(M, L, S, C, Q, W) reinterpret_cast<void (*)(const unsigned char*, unsigned char*, int, Geo)>(&pattern<M, L, S, C, Q, W>)
@@ -138,6 +152,7 @@ int main(int argc, char** argv) {
   G.bs = (unsigned)(((osz + 8 * K - 1) / (8 * K) + 15) / 16 * 16 * 8);
   G.obj = osz;
   G.nobj = (unsigned)((1ull << 30) / osz);
+  G.omap = 0;
   const unsigned BS = G.bs, NOBJ = G.nobj;
   const unsigned long long OBJ = G.obj;
   printf("# object %llu B, bs %u, %u objects\n", OBJ, BS, NOBJ);
@@ -176,6 +191,14 @@ int main(int argc, char** argv) {
       {"mixed nt wg512", PATX(0, 2, 2, 1, 1, 512), rd + wr, grid_of(1, 1, 512), 512},
       {"mixed nt wg64 cpt4", PATX(0, 2, 2, 4, 1, 64), rd + wr, grid_of(4, 1, 64), 64},
   };
+  const size_t nbase = cases.size();
+  for (size_t c = 0; c < nbase; ++c)  // every single-tile case again under the object map
+    if (cases[c].grid == grid_of(1, 1, cases[c].wg) && std::string(cases[c].name).find("seq") == std::string::npos) {
+      Case m = cases[c];
+      m.omap = 1;
+      m.name = strdup((std::string(m.name) + " objmap").c_str());
+      cases.push_back(m);
+    }
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
@@ -184,7 +207,11 @@ int main(int argc, char** argv) {
     for (size_t c = 0; c < cases.size() + 2; ++c) {
       auto launch = [&]() {
         if (c < cases.size())
-          hipLaunchKernelGGL(cases[c].k, dim3(cases[c].grid), dim3(cases[c].wg), 0, 0, in, out, 0, G);
+          {
+          Geo g = G;
+          g.omap = cases[c].omap;
+          hipLaunchKernelGGL(cases[c].k, dim3(cases[c].grid), dim3(cases[c].wg), 0, 0, in, out, 0, g);
+        }
         else if (c == cases.size())
           hipLaunchKernelGGL((flat_copy<2, 2>), dim3((unsigned)((ncopy + 255) / 256)), dim3(256), 0, 0,
                              (const u32x4*)in, (u32x4*)out, ncopy);
