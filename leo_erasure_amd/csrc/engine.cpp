@@ -333,14 +333,153 @@ int device_init() {
 
 namespace {
 
+// Host <-> device staging of the host-memory entry points (the NIF path).
+// Caller buffers are pageable (Erlang binaries), and a pageable
+// hipMemcpyAsync is a blocking copy through the runtime's own bounce buffers.
+// The measurement form LEOEC_HOST_STAGING=pinned gives each thread a small
+// pinned ring instead: the host copies chunk i+1 into a ring slot while the
+// DMA engine moves chunk i, and on the way back drains slot i while chunks
+// i+1.. are in flight (kStageSlots x chunk bytes whatever the object size).
+// It is not the default: each chunk costs ~20 us of copy submit + event
+// wait, so at 1 MiB objects it ties the pageable copies at best (1 MiB
+// chunks) and loses 1.6-2.3x at 128-256 KiB chunks
+// (profiles/r01_v14_e2e_staging.log).
+constexpr int kStageSlots = 8;
+
+int hip_ok(hipError_t e) { return e == hipSuccess ? LEOEC_OK : LEOEC_E_HIP; }
+
 struct Staging {
   int device = -1;
   hipStream_t stream = nullptr;
   uint8_t* buf = nullptr;
   size_t cap = 0;
+  uint8_t* ring = nullptr;  // pinned, kStageSlots * chunk
+  size_t chunk = 0;
+  hipEvent_t ev[kStageSlots] = {};
+  bool busy[kStageSlots] = {};
+  int next = 0;
 };
 
 thread_local Staging tl_staging;  // one stream + device buffer per calling thread
+
+bool use_pinned_ring() {
+  const char* e = std::getenv("LEOEC_HOST_STAGING");
+  return e && std::strcmp(e, "pinned") == 0;
+}
+
+size_t stage_chunk_bytes() {
+  const char* e = std::getenv("LEOEC_STAGE_CHUNK_KIB");
+  long v = e ? std::atol(e) : 256;
+  if (v < 16) v = 16;
+  if (v > 8192) v = 8192;
+  return (size_t)v << 10;
+}
+
+// Pinned ring for this thread; false = not available (use pageable copies).
+bool ring_ready(Staging* st) {
+  if (!use_pinned_ring()) return false;
+  const size_t want = stage_chunk_bytes();
+  if (st->ring && st->chunk == want) return true;
+  if (st->ring) {
+    (void)hipStreamSynchronize(st->stream);
+    (void)hipHostFree(st->ring);
+    st->ring = nullptr;
+  }
+  if (hipHostMalloc((void**)&st->ring, want * kStageSlots, hipHostMallocDefault) != hipSuccess) {
+    st->ring = nullptr;
+    return false;
+  }
+  for (int i = 0; i < kStageSlots; ++i) {
+    if (!st->ev[i] && hipEventCreateWithFlags(&st->ev[i], hipEventDisableTiming) != hipSuccess) {
+      (void)hipHostFree(st->ring);
+      st->ring = nullptr;
+      return false;
+    }
+    st->busy[i] = false;
+  }
+  st->chunk = want;
+  st->next = 0;
+  return true;
+}
+
+// Host -> device, ordered on st->stream; returns once `src` may be reused.
+int stage_h2d(Staging* st, uint8_t* dev, const uint8_t* src, size_t n) {
+  if (n == 0) return LEOEC_OK;
+  if (!ring_ready(st)) {
+    if (hipMemcpyAsync(dev, src, n, hipMemcpyHostToDevice, st->stream) != hipSuccess)
+      return LEOEC_E_HIP;
+    return LEOEC_OK;
+  }
+  for (size_t off = 0; off < n; off += st->chunk) {
+    const size_t len = std::min(st->chunk, n - off);
+    const int s = st->next;
+    st->next = (s + 1) % kStageSlots;
+    if (st->busy[s] && hipEventSynchronize(st->ev[s]) != hipSuccess) return LEOEC_E_HIP;
+    uint8_t* slot = st->ring + (size_t)s * st->chunk;
+    std::memcpy(slot, src + off, len);
+    if (hipMemcpyAsync(dev + off, slot, len, hipMemcpyHostToDevice, st->stream) != hipSuccess ||
+        hipEventRecord(st->ev[s], st->stream) != hipSuccess)
+      return LEOEC_E_HIP;
+    st->busy[s] = true;
+  }
+  return LEOEC_OK;
+}
+
+struct D2HSeg {
+  uint8_t* host;
+  const uint8_t* dev;
+  size_t n;
+};
+
+// Device -> host of every segment after the work already on st->stream, then
+// wait for the stream: on return every byte is in host memory.
+int stage_d2h_sync(Staging* st, const std::vector<D2HSeg>& segs) {
+  if (!ring_ready(st)) {
+    for (const D2HSeg& g : segs)
+      if (g.n && hipMemcpyAsync(g.host, g.dev, g.n, hipMemcpyDeviceToHost, st->stream) !=
+                     hipSuccess)
+        return LEOEC_E_HIP;
+    return hip_ok(hipStreamSynchronize(st->stream));
+  }
+  struct Piece {
+    uint8_t* host;
+    const uint8_t* dev;
+    size_t n;
+  };
+  std::vector<Piece> pc;
+  for (const D2HSeg& g : segs)
+    for (size_t off = 0; off < g.n; off += st->chunk)
+      pc.push_back(Piece{g.host + off, g.dev + off, std::min(st->chunk, g.n - off)});
+  const size_t np = pc.size();
+  std::vector<int> slot_of(np);
+  auto issue = [&](size_t i) {
+    const int s = st->next;
+    st->next = (s + 1) % kStageSlots;
+    slot_of[i] = s;
+    // the slot's previous use (an H2D chunk or an earlier piece) is ordered
+    // before this copy on the same stream; the host is done with it.
+    if (hipMemcpyAsync(st->ring + (size_t)s * st->chunk, pc[i].dev, pc[i].n,
+                       hipMemcpyDeviceToHost, st->stream) != hipSuccess ||
+        hipEventRecord(st->ev[s], st->stream) != hipSuccess)
+      return LEOEC_E_HIP;
+    st->busy[s] = true;
+    return LEOEC_OK;
+  };
+  size_t issued = 0;
+  for (; issued < np && issued < (size_t)kStageSlots; ++issued)
+    if (int rc = issue(issued)) return rc;
+  for (size_t i = 0; i < np; ++i) {
+    const int s = slot_of[i];
+    if (hipEventSynchronize(st->ev[s]) != hipSuccess) return LEOEC_E_HIP;
+    st->busy[s] = false;
+    std::memcpy(pc[i].host, st->ring + (size_t)s * st->chunk, pc[i].n);
+    if (issued < np) {
+      if (int rc = issue(issued)) return rc;
+      ++issued;
+    }
+  }
+  return hip_ok(hipStreamSynchronize(st->stream));
+}
 
 int get_staging(size_t bytes, Staging** out) {
   int rc = device_init();
@@ -399,8 +538,6 @@ void pick_survivors(int coding, int k, const int* ids, const std::vector<int>& p
     if (present[id] >= 0) { surv->push_back(id); slot->push_back(present[id]); }
 }
 
-int hip_ok(hipError_t e) { return e == hipSuccess ? LEOEC_OK : LEOEC_E_HIP; }
-
 // Stage the k survivor blocks, run the map into nwant device outputs.
 int run_host_map(const Code& c, const uint8_t* const* blocks, const std::vector<int>& surv,
                  const std::vector<int>& slot, const std::vector<int>& want, uint64_t bs,
@@ -414,7 +551,7 @@ int run_host_map(const Code& c, const uint8_t* const* blocks, const std::vector<
   std::vector<Shard> in(k), out(want.size());
   for (int i = 0; i < k; ++i) {
     uint8_t* dst = st->buf + (uint64_t)i * bs16;
-    rc = hip_ok(hipMemcpyAsync(dst, blocks[slot[i]], bs, hipMemcpyHostToDevice, st->stream));
+    rc = stage_h2d(st, dst, blocks[slot[i]], bs);
     if (rc) return rc;
     in[i] = Shard{dst, 0, bs};
   }
@@ -471,7 +608,7 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
   Staging* st;
   rc = get_staging((size_t)(k + m) * bs, &st);
   if (rc) return rc;
-  rc = hip_ok(hipMemcpyAsync(st->buf, obj, size, hipMemcpyHostToDevice, st->stream));
+  rc = stage_h2d(st, st->buf, obj, size);
   if (rc) return rc;
   std::vector<Shard> in(k), par(m);
   std::vector<int> surv(k), want(m);
@@ -485,10 +622,8 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
   }
   rc = apply(*c, surv.data(), in, want.data(), par, bs, 1, st->stream);
   if (rc) return rc;
-  rc = hip_ok(hipMemcpyAsync(out + tail_bytes, st->buf + (uint64_t)k * bs, (uint64_t)m * bs,
-                             hipMemcpyDeviceToHost, st->stream));
-  if (rc) return rc;
-  return hip_ok(hipStreamSynchronize(st->stream));
+  return stage_d2h_sync(st, {D2HSeg{out + tail_bytes, st->buf + (uint64_t)k * bs,
+                                    (size_t)((uint64_t)m * bs)}});
 }
 
 // doDecode (rscoding.cpp:87-154 and siblings): output = first `size` bytes
@@ -518,20 +653,20 @@ int op_decode(int coding, int k, int m, int w, const uint8_t* const* blocks, con
     pick_survivors(coding, k, ids, present, &surv, &slot);
     rc = run_host_map(*c, blocks, surv, slot, want, bs, &st, &dev, &dstride);
     if (rc) return rc;
-    for (size_t o = 0; o < want.size(); ++o) {
-      const uint64_t off = (uint64_t)want[o] * bs;
-      rc = hip_ok(hipMemcpyAsync(out + off, dev + o * dstride, clamp_valid(size, off, bs),
-                                 hipMemcpyDeviceToHost, st->stream));
-      if (rc) return rc;
-    }
   }
+  // surviving data blocks: host copies, overlapping the kernel
   for (int i = 0; i < k; ++i) {
     const uint64_t off = (uint64_t)i * bs;
     if (off >= size) break;
     if (present[i] >= 0) std::memcpy(out + off, blocks[present[i]], clamp_valid(size, off, bs));
   }
-  if (st) return hip_ok(hipStreamSynchronize(st->stream));
-  return LEOEC_OK;
+  if (!st) return LEOEC_OK;
+  std::vector<D2HSeg> segs;
+  for (size_t o = 0; o < want.size(); ++o) {
+    const uint64_t off = (uint64_t)want[o] * bs;
+    segs.push_back(D2HSeg{out + off, dev + o * dstride, (size_t)clamp_valid(size, off, bs)});
+  }
+  return stage_d2h_sync(st, segs);
 }
 
 // doRepair (rscoding.cpp:156-211 and siblings): blocks in repair-list order.
@@ -569,12 +704,10 @@ int op_repair(int coding, int k, int m, int w, const uint8_t* const* blocks, con
   uint64_t dstride;
   rc = run_host_map(*c, blocks, surv, slot, want, bs, &st, &dev, &dstride);
   if (rc) return rc;
-  for (size_t o = 0; o < want.size(); ++o) {
-    rc = hip_ok(hipMemcpyAsync(out + (uint64_t)pos[o] * bs, dev + o * dstride, bs,
-                               hipMemcpyDeviceToHost, st->stream));
-    if (rc) return rc;
-  }
-  return hip_ok(hipStreamSynchronize(st->stream));
+  std::vector<D2HSeg> segs;
+  for (size_t o = 0; o < want.size(); ++o)
+    segs.push_back(D2HSeg{out + (uint64_t)pos[o] * bs, dev + o * dstride, (size_t)bs});
+  return stage_d2h_sync(st, segs);
 }
 
 // ---------------------------------------------------------------------------

@@ -523,3 +523,32 @@ def test_concurrent_callers(gpu, le, oracle):
     with cf.ThreadPoolExecutor(8) as ex:
         errs = [e for e in ex.map(worker, range(8)) if e]
     assert not errs, errs
+
+
+@pytest.mark.parametrize("staging,chunk_kib", [("pinned", "16"), ("pinned", "256"),
+                                               ("pinned", "8192"), ("pageable", "256")])
+def test_host_staging_forms(gpu, le, oracle, staging, chunk_kib, monkeypatch):
+    """Host entry points (the NIF path) under both staging forms: the plain
+    pageable copies (default) and the pinned-ring measurement form (engine.cpp
+    stage_h2d / stage_d2h_sync) with chunks small enough to wrap the 8-slot
+    ring many times within one call, and one chunk per object.  Encode / decode / repair bit-exact with the
+    oracle, including ragged sizes and a 64 MiB + 5 object."""
+    monkeypatch.setenv("LEOEC_HOST_STAGING", staging)
+    monkeypatch.setenv("LEOEC_STAGE_CHUNK_KIB", chunk_kib)
+    cases = [("vandrs", 10, 4, 8, 1048576), ("vandrs", 10, 4, 8, 300001),
+             ("cauchyrs", 10, 4, 8, 1048576 + 77), ("isars", 4, 2, 8, 65536 + 7),
+             ("liberation", 4, 2, 7, 777777), ("vandrs", 6, 3, 32, 123457)]
+    if chunk_kib == "16":
+        cases.append(("vandrs", 10, 4, 8, (64 << 20) + 5))
+    for cls, k, m, w, size in cases:
+        data = rand_bytes(size, size + 17 * k)
+        ref = oracle.encode(cls, k, m, w, data)
+        st, blocks = le.nif_encode(cls, (k, m, w), data, size)
+        assert st == "ok" and blocks == ref, (cls, k, m, w, size)
+        ids = list(range(m, k + m))[::-1]
+        st, out = le.nif_decode(cls, (k, m, w), [ref[b] for b in ids], ids, size)
+        assert st == "ok" and out == data, (cls, k, m, w, size)
+        lost = [0, k + m - 1] if m > 1 else [0]
+        avail = [b for b in range(k + m) if b not in lost]
+        st, rep = le.nif_repair(cls, (k, m, w), [ref[b] for b in avail], avail, lost)
+        assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size)

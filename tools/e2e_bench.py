@@ -18,16 +18,10 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main():
+def host_paths(le, K, M, W, size, bs, filled, tag):
+    import threading
+
     import numpy as np
-    import torch
-
-    import leo_erasure_amd as le
-    torch.cuda.set_device(0)
-    assert le.gf_init() == "ok"
-    K, M, W, size = 10, 4, 8, 1 << 20
-    bs, filled = le.layout("vandrs", (K, M, W), size)
-
     # --- NIF path, pageable, one object per call
     data = np.random.default_rng(1).integers(0, 256, size, dtype=np.uint8).tobytes()
     for _ in range(3):
@@ -38,11 +32,25 @@ def main():
         st, _ = le.nif_encode("vandrs", (K, M, W), data, size)
         assert st == "ok"
     t = time.perf_counter() - t0
-    print(json.dumps({"path": "nif leoec_encode, pageable, 1 object/call, 1 thread",
+    print(json.dumps({"path": f"nif leoec_encode, 1 object/call, 1 thread [{tag}]",
+                      "GiBps": round(n * size / t / 2**30, 2), "us_per_object": round(t / n * 1e6, 1)}))
+
+    # --- NIF decode, data blocks {0,1,2,3} lost (rebuilt on the GPU), 1 thread
+    st, blocks = le.nif_encode("vandrs", (K, M, W), data, size)
+    ids = list(range(4, K + M))
+    surv = [blocks[i] for i in ids]
+    for _ in range(3):
+        le.nif_decode("vandrs", (K, M, W), surv, ids, size)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        st, out = le.nif_decode("vandrs", (K, M, W), surv, ids, size)
+        assert st == "ok"
+    t = time.perf_counter() - t0
+    assert out == data
+    print(json.dumps({"path": f"nif leoec_decode (lose 0-3), 1 object/call, 1 thread [{tag}]",
                       "GiBps": round(n * size / t / 2**30, 2), "us_per_object": round(t / n * 1e6, 1)}))
 
     # --- C ABI leoec_encode (host memory), T concurrent callers (dirty schedulers)
-    import threading
     bsz = (K + M - filled) * bs
     for T in (1, 4, 8, 16):
         per = 64
@@ -66,9 +74,32 @@ def main():
         for th in ths:
             th.join()
         t = time.perf_counter() - t0
-        print(json.dumps({"path": f"C ABI leoec_encode, pageable 1 MiB objects, {T} caller threads",
+        print(json.dumps({"path": f"C ABI leoec_encode, 1 MiB objects, {T} caller threads [{tag}]",
                           "GiBps": round(T * per * size / t / 2**30, 2),
                           "us_per_object_per_thread": round(t / per * 1e6, 1)}))
+
+
+
+def main():
+    import numpy as np
+    import torch
+
+    import leo_erasure_amd as le
+    torch.cuda.set_device(0)
+    assert le.gf_init() == "ok"
+    K, M, W, size = 10, 4, 8, 1 << 20
+    bs, filled = le.layout("vandrs", (K, M, W), size)
+
+    # Host staging forms of the host entry points (engine.cpp): the pinned
+    # ring at several chunk sizes, and plain pageable copies.
+    forms = [("pageable", "256"), ("pinned", "128"), ("pinned", "256"), ("pinned", "512"),
+             ("pinned", "1024")]
+    if len(sys.argv) > 1 and sys.argv[1] == "--quick":
+        forms = [("pageable", "256"), ("pinned", "256")]
+    for staging, ck in forms:
+        os.environ["LEOEC_HOST_STAGING"] = staging
+        os.environ["LEOEC_STAGE_CHUNK_KIB"] = ck
+        host_paths(le, K, M, W, size, bs, filled, f"{staging}/{ck}KiB")
 
     # --- pinned, batched, two streams
     total, chunk = 1024, 64
