@@ -358,13 +358,58 @@ struct Staging {
   hipEvent_t ev[kStageSlots] = {};
   bool busy[kStageSlots] = {};
   int next = 0;
+  uint8_t* hbuf = nullptr;  // pinned, gather form
+  size_t hcap = 0;
 };
 
 thread_local Staging tl_staging;  // one stream + device buffer per calling thread
 
-bool use_pinned_ring() {
+// Default (auto): gather when a direction has several separate host buffers
+// (decode / repair: k survivor binaries in, e rebuilt blocks out), pageable
+// for one contiguous buffer (encode), measured best on each
+// (profiles/r01_v14_e2e_gather.log).  "gather" / "pageable" / "pinned" force
+// one form.
+enum class StageForm { kAuto, kPageable, kGather, kRing };
+
+StageForm stage_form() {
   const char* e = std::getenv("LEOEC_HOST_STAGING");
-  return e && std::strcmp(e, "pinned") == 0;
+  if (!e) return StageForm::kAuto;
+  if (std::strcmp(e, "pinned") == 0) return StageForm::kRing;
+  if (std::strcmp(e, "gather") == 0) return StageForm::kGather;
+  if (std::strcmp(e, "pageable") == 0) return StageForm::kPageable;
+  return StageForm::kAuto;
+}
+
+bool gather_wanted(size_t nsegs) {
+  const StageForm f = stage_form();
+  return f == StageForm::kGather || (f == StageForm::kAuto && nsegs > 1);
+}
+
+bool use_pinned_ring() { return stage_form() == StageForm::kRing; }
+
+// Gather form: one pinned buffer per thread holding a whole call's blocks,
+// so a call moves its k input blocks in ONE copy and its outputs in ONE copy
+// (host memcpys pack / unpack the caller's separate binaries).  Spans above
+// kGatherMax go through the pageable copies (large copies amortise their
+// submit cost anyway, and 64 MiB objects should not pin ~100 MB per thread).
+constexpr size_t kGatherMax = (size_t)16 << 20;
+
+uint8_t* gather_buf(Staging* st, size_t bytes) {
+  if (bytes == 0 || bytes > kGatherMax) return nullptr;
+  if (st->hcap >= bytes) return st->hbuf;
+  if (st->hbuf) {
+    (void)hipStreamSynchronize(st->stream);
+    (void)hipHostFree(st->hbuf);
+    st->hbuf = nullptr;
+    st->hcap = 0;
+  }
+  const size_t want = std::max<size_t>(bytes + bytes / 4, (size_t)2 << 20);
+  if (hipHostMalloc((void**)&st->hbuf, want, hipHostMallocDefault) != hipSuccess) {
+    st->hbuf = nullptr;
+    return nullptr;
+  }
+  st->hcap = want;
+  return st->hbuf;
 }
 
 size_t stage_chunk_bytes() {
@@ -425,6 +470,25 @@ int stage_h2d(Staging* st, uint8_t* dev, const uint8_t* src, size_t n) {
   return LEOEC_OK;
 }
 
+struct H2DSeg {
+  const uint8_t* host;
+  size_t dev_off;  // from the device base
+  size_t n;
+};
+
+// Host -> device of every segment into dev_base, ordered on st->stream.
+int stage_h2d_segs(Staging* st, uint8_t* dev_base, const std::vector<H2DSeg>& segs) {
+  size_t span = 0;
+  for (const H2DSeg& g : segs) span = std::max(span, g.dev_off + g.n);
+  if (uint8_t* hb = gather_wanted(segs.size()) ? gather_buf(st, span) : nullptr) {
+    for (const H2DSeg& g : segs) std::memcpy(hb + g.dev_off, g.host, g.n);
+    return hip_ok(hipMemcpyAsync(dev_base, hb, span, hipMemcpyHostToDevice, st->stream));
+  }
+  for (const H2DSeg& g : segs)
+    if (int rc = stage_h2d(st, dev_base + g.dev_off, g.host, g.n)) return rc;
+  return LEOEC_OK;
+}
+
 struct D2HSeg {
   uint8_t* host;
   const uint8_t* dev;
@@ -434,6 +498,22 @@ struct D2HSeg {
 // Device -> host of every segment after the work already on st->stream, then
 // wait for the stream: on return every byte is in host memory.
 int stage_d2h_sync(Staging* st, const std::vector<D2HSeg>& segs) {
+  if (gather_wanted(segs.size()) && !segs.empty()) {
+    const uint8_t* lo = segs[0].dev;
+    const uint8_t* hi = segs[0].dev;
+    for (const D2HSeg& g : segs) {
+      lo = std::min(lo, g.dev);
+      hi = std::max(hi, g.dev + g.n);
+    }
+    if (uint8_t* hb = gather_buf(st, (size_t)(hi - lo))) {
+      if (hipMemcpyAsync(hb, lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, st->stream) !=
+              hipSuccess ||
+          hipStreamSynchronize(st->stream) != hipSuccess)
+        return LEOEC_E_HIP;
+      for (const D2HSeg& g : segs) std::memcpy(g.host, hb + (g.dev - lo), g.n);
+      return LEOEC_OK;
+    }
+  }
   if (!ring_ready(st)) {
     for (const D2HSeg& g : segs)
       if (g.n && hipMemcpyAsync(g.host, g.dev, g.n, hipMemcpyDeviceToHost, st->stream) !=
@@ -549,12 +629,13 @@ int run_host_map(const Code& c, const uint8_t* const* blocks, const std::vector<
   int rc = get_staging((size_t)(k + want.size()) * bs16, &st);
   if (rc) return rc;
   std::vector<Shard> in(k), out(want.size());
+  std::vector<H2DSeg> segs(k);
   for (int i = 0; i < k; ++i) {
-    uint8_t* dst = st->buf + (uint64_t)i * bs16;
-    rc = stage_h2d(st, dst, blocks[slot[i]], bs);
-    if (rc) return rc;
-    in[i] = Shard{dst, 0, bs};
+    segs[i] = H2DSeg{blocks[slot[i]], (size_t)((uint64_t)i * bs16), (size_t)bs};
+    in[i] = Shard{st->buf + (uint64_t)i * bs16, 0, bs};
   }
+  rc = stage_h2d_segs(st, st->buf, segs);
+  if (rc) return rc;
   uint8_t* outbase = st->buf + (uint64_t)k * bs16;
   for (size_t o = 0; o < want.size(); ++o) out[o] = Shard{outbase + o * bs16, 0, bs};
   rc = apply(c, surv.data(), in, want.data(), out, bs16, 1, st->stream);
@@ -608,7 +689,7 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
   Staging* st;
   rc = get_staging((size_t)(k + m) * bs, &st);
   if (rc) return rc;
-  rc = stage_h2d(st, st->buf, obj, size);
+  rc = stage_h2d_segs(st, st->buf, {H2DSeg{obj, 0, (size_t)size}});
   if (rc) return rc;
   std::vector<Shard> in(k), par(m);
   std::vector<int> surv(k), want(m);

@@ -92,10 +92,9 @@ def main():
 
     # Host staging forms of the host entry points (engine.cpp): the pinned
     # ring at several chunk sizes, and plain pageable copies.
-    forms = [("pageable", "256"), ("pinned", "128"), ("pinned", "256"), ("pinned", "512"),
-             ("pinned", "1024")]
+    forms = [("auto", "256"), ("pageable", "256"), ("gather", "256"), ("pinned", "1024")]
     if len(sys.argv) > 1 and sys.argv[1] == "--quick":
-        forms = [("pageable", "256"), ("pinned", "256")]
+        forms = [("auto", "256"), ("pageable", "256")]
     for staging, ck in forms:
         os.environ["LEOEC_HOST_STAGING"] = staging
         os.environ["LEOEC_STAGE_CHUNK_KIB"] = ck
