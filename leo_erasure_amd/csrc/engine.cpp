@@ -12,6 +12,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <tuple>
 
 #include "../../include/leoec.h"
@@ -360,7 +361,43 @@ struct Staging {
   int next = 0;
   uint8_t* hbuf = nullptr;  // pinned, gather form
   size_t hcap = 0;
+
+  Staging() = default;
+  Staging(const Staging&) = delete;
+  Staging& operator=(const Staging&) = delete;
+  // A caller thread that exits (a dirty scheduler torn down, a thread pool
+  // shrinking) gives back its stream, device buffer and pinned buffers.  The
+  // thread that loaded the library is skipped: its thread_local storage dies
+  // during process exit, when the HIP runtime may already be going away.
+  ~Staging() {
+    if (std::this_thread::get_id() != load_thread()) release();
+  }
+  void release() {
+    if (device >= 0 && stream) {
+      (void)hipSetDevice(device);
+      (void)hipStreamSynchronize(stream);
+      for (hipEvent_t& e : ev)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
+      if (buf) (void)hipFree(buf);
+      if (ring) (void)hipHostFree(ring);
+      if (hbuf) (void)hipHostFree(hbuf);
+      (void)hipStreamDestroy(stream);
+    }
+    device = -1;
+    stream = nullptr;
+    buf = ring = hbuf = nullptr;
+    cap = chunk = hcap = 0;
+    for (bool& b : busy) b = false;
+    next = 0;
+  }
+  static std::thread::id load_thread() {
+    static const std::thread::id id = std::this_thread::get_id();
+    return id;
+  }
 };
+
+// Record the loading thread at library load (static initialisation).
+const std::thread::id g_load_thread = Staging::load_thread();
 
 thread_local Staging tl_staging;  // one stream + device buffer per calling thread
 
@@ -568,7 +605,10 @@ int get_staging(size_t bytes, Staging** out) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return LEOEC_E_HIP;
   if (st.device != dev) {
-    st = Staging();
+    if (st.device >= 0) {
+      st.release();  // buffers of the previous device (release() selects it)
+      if (hipSetDevice(dev) != hipSuccess) return LEOEC_E_HIP;
+    }
     if (hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking) != hipSuccess)
       return LEOEC_E_HIP;
     st.device = dev;

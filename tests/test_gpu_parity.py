@@ -559,3 +559,45 @@ def test_host_staging_forms(gpu, le, oracle, staging, chunk_kib, monkeypatch):
         avail = [b for b in range(k + m) if b not in lost]
         st, rep = le.nif_repair(cls, (k, m, w), [ref[b] for b in avail], avail, lost)
         assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size)
+
+
+def test_thread_exit_releases_staging(gpu, le, oracle):
+    """Caller threads that come and go (dirty schedulers, pools) give back their
+    per-thread stream, device buffer and pinned buffers (engine.cpp
+    Staging::release): 160 short-lived threads each run a decode (gather
+    staging) + encode of an 8 MiB object; device memory must not drift by
+    their buffers (~19 MB each would be ~3 GB)."""
+    import threading
+
+    import torch
+
+    k, m, w, size = 10, 4, 8, 8 << 20
+    data = rand_bytes(size, 4242)
+    ref = oracle.encode("vandrs", k, m, w, data)
+    ids = list(range(4, k + m))
+    errs = []
+
+    def one():
+        st, out = le.nif_decode("vandrs", (k, m, w), [ref[b] for b in ids], ids, size)
+        if st != "ok" or out != data:
+            errs.append("decode")
+        st, blocks = le.nif_encode("vandrs", (k, m, w), data, size)
+        if st != "ok" or blocks != ref:
+            errs.append("encode")
+
+    def wave(n):
+        ths = [threading.Thread(target=one) for _ in range(n)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+
+    wave(8)  # runtime warm-up
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info()
+    for _ in range(20):
+        wave(8)
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info()
+    assert not errs, errs[:4]
+    assert free0 - free1 < (512 << 20), (free0 - free1) / 2**20

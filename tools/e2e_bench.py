@@ -57,20 +57,25 @@ def host_paths(le, K, M, W, size, bs, filled, tag):
         srcs = [np.random.default_rng(t).integers(0, 256, size, dtype=np.uint8) for t in range(T)]
         outs = [np.empty(bsz, dtype=np.uint8) for _ in range(T)]
 
+        ready = threading.Barrier(T + 1)
+        go = threading.Event()
+
         def work(t):
+            # warm this thread's stream / staging buffers outside the timed region
+            rc = le.lib.leoec_encode(2, K, M, W, srcs[t].ctypes.data, size, outs[t].ctypes.data, bsz)
+            assert rc == 0
+            ready.wait()
+            go.wait()
             for _ in range(per):
                 rc = le.lib.leoec_encode(2, K, M, W, srcs[t].ctypes.data, size, outs[t].ctypes.data, bsz)
                 assert rc == 0
 
-        for t in range(T):  # warm each thread's stream / staging
-            work_t = threading.Thread(target=lambda: le.lib.leoec_encode(
-                2, K, M, W, srcs[0].ctypes.data, size, outs[0].ctypes.data, bsz))
-            work_t.start()
-            work_t.join()
         ths = [threading.Thread(target=work, args=(t,)) for t in range(T)]
-        t0 = time.perf_counter()
         for th in ths:
             th.start()
+        ready.wait()
+        t0 = time.perf_counter()
+        go.set()
         for th in ths:
             th.join()
         t = time.perf_counter() - t0
