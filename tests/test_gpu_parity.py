@@ -601,3 +601,36 @@ def test_thread_exit_releases_staging(gpu, le, oracle):
     free1, _ = torch.cuda.mem_get_info()
     assert not errs, errs[:4]
     assert free0 - free1 < (512 << 20), (free0 - free1) / 2**20
+
+
+def test_default_w_substitution(gpu, le):
+    """suite_test_'s W = -1 and W = 0 cases (test/leo_erasure_tests.erl:40-48):
+    encode/3 and decode/4 substitute ?coding_params_w(Class)
+    (src/leo_erasure.erl:155-156,203-204); the blocks equal an explicit-W
+    encode and decode with the substituted W round-trips."""
+    data = rand_bytes(300001, 40)
+    for cls, k, m in [("vandrs", 10, 4), ("cauchyrs", 4, 2), ("liberation", 4, 2), ("isars", 10, 4)]:
+        w = le.api.coding_params_w(cls)
+        st, ref = le.encode(cls, (k, m, w), data)
+        assert st == "ok"
+        for bad_w in (-1, 0):
+            st, idb = le.encode(cls, (k, m, bad_w), data)
+            assert st == "ok" and idb == ref, (cls, bad_w)
+            keep = idb[m:]  # lose the first m blocks
+            assert le.decode(cls, (k, m, bad_w), keep, len(data)) == ("ok", data), (cls, bad_w)
+
+
+def test_bench_encode_100MiB_zero(gpu, le):
+    """bench_encode_test (test/leo_erasure_tests.erl:207-212,304-336): one
+    encode of a 100 MiB all-zero binary per class.  Every code is linear, so
+    every block is zero; a decode from the last k blocks returns the object."""
+    size = 100 << 20
+    data = bytes(size)
+    for cls, k, m, w in [("vandrs", 10, 4, 8), ("cauchyrs", 4, 2, 3), ("liberation", 4, 2, 7),
+                         ("isars", 10, 4, 8)]:
+        st, blocks = le.nif_encode(cls, (k, m, w), data, size)
+        assert st == "ok" and len(blocks) == k + m
+        assert all(not any(b[::4096]) and b.count(0) == len(b) for b in blocks[k:]), cls
+        ids = list(range(m, k + m))
+        st, out = le.nif_decode(cls, (k, m, w), [blocks[i] for i in ids], ids, size)
+        assert st == "ok" and out == data, cls
