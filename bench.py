@@ -38,7 +38,7 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=100)
-    p.add_argument("--objects", type=int, default=1024, help="1 MiB objects per GPU")
+    p.add_argument("--objects", type=int, default=2048, help="1 MiB objects per GPU (one launch)")
     p.add_argument("--size", type=int, default=1048576)
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="target CPU time of the bounded cpu_baseline sample")

@@ -52,4 +52,5 @@ def main(out_dir, objects=1024, object_bytes=1048576, block_size=104960):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out")
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out",
+         int(sys.argv[2]) if len(sys.argv) > 2 else 2048)
