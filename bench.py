@@ -1,19 +1,34 @@
 """Headline benchmark: device-resident encode+decode GiB/s, vandrs RS(10,4,8),
-1 MiB objects (BASELINE.json metric / configs[1..2]).
+1 MiB objects (BASELINE.json metric / configs[1..2]), plus the configs[4]
+partitioned 64 MiB batch.
 
 One step = encode every object of this rank's batch (10 data blocks read, 4
 coding blocks written per object) + in-place decode of the same batch with
-data blocks {0,1,2,3} erased (6 data + 4 coding read, 4 data written).
-Objects are independent, so N GPUs = N processes with their own batches and
-no collectives on the data path (weak scaling); a barrier and a max-reduce of
-the elapsed time bracket the timed region.
+data blocks {0,1,2,3} erased (6 data + 4 coding read, 4 data written).  The
+reference's unit of work is one independent object per call
+(`c_src/rscoding.cpp:36-85`), so N GPUs = N processes with their own objects
+and no collective on the data path:
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N > 1: launched by torch.distributed.run, one rank per GPU)
+* ``--workload 1MiB`` (default): every rank owns ``--objects`` 1 MiB objects
+  (weak scaling, the BASELINE metric);
+* ``--workload 64MiB``: one global batch of 64 x 64 MiB objects split over the
+  ranks with `shard_range` (strong scaling, BASELINE configs[4]).
+
+Control traffic (a barrier around the timed region, the max over ranks of
+the elapsed time, each rank's verification verdict) goes over gloo on the
+host: the data path has no collective and the bench needs no RCCL.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 1MiB|64MiB]
+  N > 1 without WORLD_SIZE in the environment: this process starts N ranks
+  (torch.distributed.run) before touching the GPU and exits with their
+  status; under a launcher each rank maps LOCAL_RANK to one device.
 """
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -21,9 +36,20 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s device-resident encode+decode, vandrs RS(10,4,w=8) 1 MiB objects"
+METRIC_64 = "GiB/s device-resident encode+decode, vandrs RS(10,4,w=8) 64 MiB objects, partitioned batch"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 K, M, W = 10, 4, 8
-ERASED = [0, 1, 2, 3]
+ERASED = [0, 1, 2, 3]          # the timed decode: worst case, 4 data blocks rebuilt
+VERIFY_ERASED = [4, 7, 9, 10]  # a second pattern for the check: tail block, parity 11..13 used
+POISON = 0xA5
+WORKLOADS = {
+    # name: (object bytes, objects per rank or None, global objects or None)
+    "1MiB": (1 << 20, 2048, None),
+    "64MiB": (64 << 20, None, 64),
+}
+# The GPU box grants one GPU's process 16 CPUs (the harness's CPU share);
+# nproc / affinity there show the whole host.  Used when no cgroup quota says.
+BOX_CPU_SHARE = 16
 
 
 def shard_range(rank, world, total):
@@ -38,179 +64,353 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=100)
-    p.add_argument("--objects", type=int, default=2048, help="1 MiB objects per GPU (one launch)")
-    p.add_argument("--size", type=int, default=1048576)
+    p.add_argument("--warmup-s", type=float, default=1.0,
+                   help="minimum warm-up wall time (clock ramp); at least --warmup steps run")
+    p.add_argument("--workload", choices=sorted(WORKLOADS), default="1MiB")
+    p.add_argument("--objects", type=int, default=None,
+                   help="1MiB: objects per GPU (one launch); 64MiB: global batch")
+    p.add_argument("--size", type=int, default=None, help="object bytes (default: the workload's)")
+    p.add_argument("--oversubscribe", action="store_true",
+                   help="allow more ranks than devices (ranks share devices; rehearsal only)")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="target CPU time of the bounded cpu_baseline sample")
+    p.add_argument("--cpu-objects", type=int, default=1024,
+                   help="objects in the cpu_baseline sample (copied from rank 0's batch)")
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     return p.parse_args(argv)
 
 
-def cpu_baseline(size, target_s, threads, sample_objs=2048):
-    """The CPU restatement with ISA-L's split-table (PSHUFB) technique, timed on
-    this host's cores over a bounded sample of the same workload: a 2 GiB
-    batch (beyond any host LLC) encoded + decoded in repeated passes until
-    about `target_s` seconds of wall time have been spent."""
+# ---------------------------------------------------------------------------
+# Device backend: the measured path.
+class GpuBackend:
+    """libleoec's device entry points (leoec_encode_dev / leoec_decode_dev) on
+    this rank's GPU; work is enqueued on torch's current stream."""
+
+    def __init__(self, local_rank, world, oversubscribe=False):
+        import torch
+
+        import leo_erasure_amd as le
+
+        ndev = torch.cuda.device_count()
+        if ndev <= 0:
+            raise SystemExit("bench.py: no GPU visible")
+        if world > ndev and not oversubscribe:
+            raise SystemExit(f"bench.py: {world} ranks but {ndev} device(s); "
+                             "pass --oversubscribe to share devices")
+        self.index = local_rank % ndev
+        torch.cuda.set_device(self.index)
+        st = le.gf_init()
+        if st != "ok":
+            raise SystemExit(f"bench.py: gf_init -> {st}")
+        self.torch = torch
+        self.le = le
+        self.device = torch.device("cuda", self.index)
+        self.name = f"cuda:{self.index} {torch.cuda.get_device_name(self.index)}"
+
+    def random_batch(self, n, size, seed):
+        t = self.torch
+        gen = t.Generator(device=self.device).manual_seed(seed)
+        return t.randint(0, 256, (n, size), dtype=t.uint8, device=self.device, generator=gen)
+
+    def empty(self, n, cols):
+        return self.torch.empty((n, cols), dtype=self.torch.uint8, device=self.device)
+
+    def encode(self, objs, size, parity):
+        self.le.device.encode("vandrs", (K, M, W), objs, size, parity)
+
+    def decode(self, objs, size, parity, erased):
+        self.le.device.decode("vandrs", (K, M, W), objs, size, parity, erased)
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def event(self):
+        return self.torch.cuda.Event(enable_timing=True)
+
+
+# ---------------------------------------------------------------------------
+def cpu_share():
+    """Threads the CPU baseline may use on this host, and what that rests on."""
+    host = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = host
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, period = fh.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        quota = None
+    if quota:
+        threads, basis = max(1, min(aff, int(math.floor(quota)))), "cgroup cpu.max quota"
+    else:
+        threads, basis = min(aff, BOX_CPU_SHARE), (
+            f"affinity, capped at {BOX_CPU_SHARE} = the GPU box's CPU share per GPU")
+    return threads, {"host_cpus": host, "affinity_cpus": aff, "cgroup_cpus": quota,
+                     "threads_basis": basis}
+
+
+def cpu_baseline(objs, parity, size, n_sample, target_s):
+    """The CPU restatement with ISA-L's split-table / GFNI technique
+    (oracle/leoec_oracle.c orc_bench_rs8), timed on this host's cores over a
+    bounded sample of the SAME workload: the first `n_sample` objects of rank
+    0's batch, copied to host memory.  Its encode output is also compared
+    byte for byte with the GPU's parity of those objects (outside the timed
+    region), so the line's `verified` covers encode parity too."""
     import numpy as np
 
     from oracle import oracle as O
 
-    bs = O.block_size(K, W, size)
-    n = sample_objs
-    rng = np.random.Generator(np.random.PCG64(0x1E0E))
-    objs = rng.integers(0, 256, (n, size), dtype=np.uint8)
-    parity = np.zeros((n, M * bs), dtype=np.uint8)
-    te = td = 0.0
-    passes = 0
-    while te + td < target_s or passes == 0:
+    threads, share = cpu_share()
+    n = min(n_sample, objs.shape[0])
+    host = objs[:n].to("cpu", copy=True).numpy()
+    gpu_par = parity[:n].to("cpu", copy=True).numpy()
+    cpu_par = np.zeros_like(gpu_par)
+    O.bench_rs8(0, K, M, host, size, size, n, cpu_par, threads=threads)
+    parity_ok = bool(np.array_equal(cpu_par, gpu_par))
+    rates = []
+    t_all = 0.0
+    while t_all < target_s or len(rates) < 3:
         t0 = time.perf_counter()
-        O.bench_rs8(0, K, M, objs, size, size, n, parity, threads=threads)
-        t1 = time.perf_counter()
-        O.bench_rs8(1, K, M, objs, size, size, n, parity, erased=ERASED, threads=threads)
-        t2 = time.perf_counter()
-        te += t1 - t0
-        td += t2 - t1
-        passes += 1
-    gib = 2 * n * passes * size / (te + td) / 2**30
-    return {
-        "value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        O.bench_rs8(0, K, M, host, size, size, n, cpu_par, threads=threads)
+        O.bench_rs8(1, K, M, host, size, size, n, cpu_par, erased=ERASED, threads=threads)
+        dt = time.perf_counter() - t0
+        t_all += dt
+        rates.append(2 * n * size / dt / 2**30)
+    rates.sort()
+    med = rates[len(rates) // 2]
+    rec = {
+        "value": round(med, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
         "simd": {0: "scalar", 2: "avx2-pshufb (ISA-L split tables)",
                  3: "avx512-gfni (ISA-L gf2p8affine)"}.get(O.simd_level(), "scalar"),
-        "sample": f"{passes} passes over {n} x {size} B objects: vandrs RS({K},{M},8) encode "
-                  f"{te:.2f} s + in-place decode of data blocks {ERASED} {td:.2f} s, "
-                  f"{threads} threads",
+        "sample": f"{len(rates)} passes over the first {n} x {size} B objects of rank 0's batch: "
+                  f"vandrs RS({K},{M},8) encode + in-place decode of data blocks {ERASED}, "
+                  f"{threads} threads, {t_all:.2f} s; value = median pass",
+        "pass_spread": round((rates[-1] - rates[0]) / med, 4) if med else None,
+        "iqr_spread": round((rates[(3 * len(rates)) // 4] - rates[len(rates) // 4]) / med, 4)
+        if med else None,
+        "parity_vs_gpu": {"objects": n, "equal": parity_ok},
     }
+    rec.update(share)
+    return rec
 
 
-def main(argv=None):
-    args = parse(argv)
-    import torch
-    import torch.distributed as dist
+# ---------------------------------------------------------------------------
+def _poison_decode(be, objs, ref, parity, size, bs, erased):
+    """Overwrite the erased data blocks, rebuild them, require the batch to
+    equal its pristine copy: a decode that writes nothing fails this."""
+    for b in erased:
+        if b >= K:
+            continue
+        lo, hi = b * bs, min((b + 1) * bs, size)
+        if lo < hi:
+            objs[:, lo:hi] = POISON
+    be.decode(objs, size, parity, erased)
+    be.sync()
+    return bool(objs.equal(ref))
 
-    import leo_erasure_amd as le
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+def run_rank(args, be, rank, world, dist=None):
+    """One rank of the bench; returns (record-or-None, verified)."""
+    size = args.size or WORKLOADS[args.workload][0]
+    per_rank, global_n = WORKLOADS[args.workload][1:]
+    if args.objects is not None:
+        if global_n is None:
+            per_rank = args.objects
+        else:
+            global_n = args.objects
+    if global_n is not None:
+        lo, hi = shard_range(rank, world, global_n)
     else:
-        torch.cuda.set_device(0)
-    assert le.gf_init() == "ok", le.gf_init()
-    dev = torch.device("cuda", torch.cuda.current_device())
+        lo, hi = rank * per_rank, (rank + 1) * per_rank
+    n = hi - lo
+    bs = ((size + K * W - 1) // (K * W) + 15) // 16 * 16 * W  # rscoding.cpp:44
+    if n <= 0:
+        raise SystemExit(f"rank {rank}: no objects (global batch {global_n}, {world} ranks)")
 
-    size, n = args.size, args.objects
-    bs, _ = le.layout("vandrs", (K, M, W), size)
-    gen = torch.Generator(device=dev).manual_seed(0x1E0E + rank)
-    objs = torch.randint(0, 256, (n, size), dtype=torch.uint8, device=dev, generator=gen)
-    parity = torch.empty((n, M * bs), dtype=torch.uint8, device=dev)
+    objs = be.random_batch(n, size, 0x1E0E + lo)
+    parity = be.empty(n, M * bs)
     ref = objs.clone()
-    stream = torch.cuda.current_stream()
 
     def step(ev=None):
         if ev is not None:
-            ev[0].record(stream)
-        le.device.encode("vandrs", (K, M, W), objs, size, parity)
+            ev[0].record()
+        be.encode(objs, size, parity)
         if ev is not None:
-            ev[1].record(stream)
-        le.device.decode("vandrs", (K, M, W), objs, size, parity, ERASED)
+            ev[1].record()
+        be.decode(objs, size, parity, ERASED)
         if ev is not None:
-            ev[2].record(stream)
+            ev[2].record()
 
-    for _ in range(args.warmup):
+    # warm-up: at least W steps and at least --warmup-s seconds (clock ramp)
+    tw = time.perf_counter()
+    wsteps = 0
+    while wsteps < args.warmup or time.perf_counter() - tw < args.warmup_s:
         step()
-    torch.cuda.synchronize()
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
+        wsteps += 1
+        if wsteps % 16 == 0:
+            be.sync()
+    be.sync()
+    warm_s = time.perf_counter() - tw
+
+    events = [[be.event() for _ in range(3)] for _ in range(args.steps)]
+    be.sync()
+    if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    be.sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(events[i])
-    torch.cuda.synchronize()
-    if world > 1:
+    be.sync()
+    if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
 
     enc_t = [e[0].elapsed_time(e[1]) for e in events]
     dec_t = [e[1].elapsed_time(e[2]) for e in events]
-    enc_ms = sum(enc_t) / args.steps
-    dec_ms = sum(dec_t) / args.steps
-    # decode rebuilt blocks 0..3 in place every step: the batch must be intact
-    intact = bool(torch.equal(objs, ref))
-    if world > 1:
-        f = torch.tensor([0 if intact else 1], device=dev)
-        dist.all_reduce(f, op=dist.ReduceOp.MAX)
-        intact = f.item() == 0
+    enc_ms = sum(enc_t) / len(enc_t)
+    dec_ms = sum(dec_t) / len(dec_t)
 
-    if rank == 0:
-        total_objs = n * world
-        value = 2.0 * total_objs * size * args.steps / elapsed / 2**30
-        enc_bytes = (K + M) * bs * n              # algorithmic bytes per encode launch
-        dec_bytes = (K + len(ERASED)) * bs * n    # per decode launch
-        enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
-        dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
-        traffic = None
-        if os.path.exists(args.traffic):
-            try:
-                with open(args.traffic) as fh:
-                    tr = json.load(fh)
-                if tr.get("objects") == n and tr.get("object_bytes") == size:
-                    traffic = tr.get("encode_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
-        rec = {
-            "metric": METRIC,
-            "value": round(value, 3),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (uniform random bytes, torch Philox seed 0x1E0E+rank)",
-            "config": {
-                "workload": "vandrs RS(k=10,m=4,w=8) encode + in-place decode of data blocks "
-                            "{0,1,2,3}, 1 MiB objects, device-resident batch",
-                "objects_per_gpu": n, "object_bytes": size, "block_size": bs,
-                "parallelism": f"object-sharded x{world}, no collectives",
-            },
-            "roofline": {
-                "bound": "hbm", "kernel": "gf8_apply<10,4> (encode)",
-                "achieved": round(enc_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(enc_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "alg_bytes_per_launch": enc_bytes, "avg_launch_ms": round(enc_ms, 4),
-                "decode": {"achieved": round(dec_gbs, 1), "frac": round(dec_gbs / HBM_PEAK_GBS, 4),
-                           "alg_bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_ms, 4)},
-            },
-            "kernel_ms": {"encode_min_med_max": [round(x, 4) for x in (min(enc_t), sorted(enc_t)[len(enc_t) // 2], max(enc_t))],
-                          "decode_min_med_max": [round(x, 4) for x in (min(dec_t), sorted(dec_t)[len(dec_t) // 2], max(dec_t))]},
-            "verified": intact,
-        }
-        if world == 1 and not args.no_cpu:
-            try:
-                threads = min(16, len(os.sched_getaffinity(0)))
-            except AttributeError:
-                threads = min(16, os.cpu_count() or 1)
-            rec["cpu_baseline"] = cpu_baseline(size, args.cpu_seconds, threads)
-        else:
-            rec["cpu_baseline"] = None
-        print(json.dumps(rec), flush=True)
+    # verification, outside the timed region
+    intact = bool(objs.equal(ref))                       # the timed decodes kept the batch
+    dec_ok = _poison_decode(be, objs, ref, parity, size, bs, ERASED)
+    dec2_ok = _poison_decode(be, objs, ref, parity, size, bs, VERIFY_ERASED)
+    mine = {"rank": rank, "device": getattr(be, "name", "?"), "objects": [lo, hi],
+            "elapsed_s": elapsed, "enc_ms": enc_ms, "dec_ms": dec_ms,
+            "warmup_steps": wsteps, "warmup_s": warm_s,
+            "checks": {"timed_batch_intact": intact, "poisoned_decode_0_1_2_3": dec_ok,
+                       "poisoned_decode_4_7_9_10": dec2_ok}}
+    if dist is not None:
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+    else:
+        allr = [mine]
+    verified = all(all(r["checks"].values()) for r in allr)
+    if rank != 0:
+        return None, verified
+
+    el = max(r["elapsed_s"] for r in allr)
+    total_objs = sum(r["objects"][1] - r["objects"][0] for r in allr)
+    value = 2.0 * total_objs * size * args.steps / el / 2**30
+    enc_bytes = (K + M) * bs * n              # algorithmic bytes per encode launch (rank 0)
+    dec_bytes = (K + len(ERASED)) * bs * n    # per decode launch
+    enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
+    dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            with open(args.traffic) as fh:
+                tr = json.load(fh)
+            if tr.get("objects") == n and tr.get("object_bytes") == size:
+                traffic = tr.get("encode_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    strong = global_n is not None
+    rec = {
+        "metric": METRIC_64 if strong else METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "warmup_steps_run": wsteps,
+        "warmup_s": round(warm_s, 3),
+        "ms_per_step": round(el / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong" if strong else "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (uniform random bytes, torch Philox, seed 0x1E0E + first object index)",
+        "config": {
+            "workload": (f"vandrs RS(k=10,m=4,w=8) encode + in-place decode of data blocks "
+                         f"{{0,1,2,3}}, {size} B objects, device-resident batch"
+                         + (f", global batch of {global_n} objects partitioned over the ranks"
+                            if strong else "")),
+            "objects_per_gpu": n if not strong else None,
+            "global_objects": total_objs, "object_bytes": size, "block_size": bs,
+            "parallelism": f"object-sharded x{world}, no data-path collective (gloo control only)",
+        },
+        "roofline": {
+            "bound": "hbm", "kernel": "gf8_apply<10,4> (encode)",
+            "achieved": round(enc_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(enc_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "alg_bytes_per_launch": enc_bytes, "avg_launch_ms": round(enc_ms, 4),
+            "decode": {"achieved": round(dec_gbs, 1), "frac": round(dec_gbs / HBM_PEAK_GBS, 4),
+                       "alg_bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_ms, 4)},
+        },
+        "kernel_ms": {
+            "encode_min_med_max": [round(x, 4) for x in (min(enc_t), sorted(enc_t)[len(enc_t) // 2],
+                                                         max(enc_t))],
+            "decode_min_med_max": [round(x, 4) for x in (min(dec_t), sorted(dec_t)[len(dec_t) // 2],
+                                                         max(dec_t))]},
+        "per_rank": [{"rank": r["rank"], "device": r["device"], "objects": r["objects"],
+                      "elapsed_s": round(r["elapsed_s"], 5),
+                      "encode_ms": round(r["enc_ms"], 4), "decode_ms": round(r["dec_ms"], 4),
+                      "checks": r["checks"]} for r in allr],
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu:
+        # parity holds the last timed encode of the pristine batch (`ref`)
+        cb = cpu_baseline(ref, parity, size, args.cpu_objects, args.cpu_seconds)
+        rec["cpu_baseline"] = cb
+        verified = verified and cb["parity_vs_gpu"]["equal"]
+    rec["verified"] = verified
+    return rec, verified
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """Start `--gpus` ranks of this script under torch.distributed.run as a
+    child process (this process never touches the GPU) and return its status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)]
+    cmd += list(sys.argv[1:] if argv is None else argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def main(argv=None, backend=GpuBackend):
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            return launch_ranks(args, argv)
+        world, rank, local = 1, 0, 0
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    dist = None
     if world > 1:
-        dist.destroy_process_group()
-    if not intact:
-        sys.exit(1)
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        be = backend(local, world, args.oversubscribe)
+        rec, verified = run_rank(args, be, rank, world, dist)
+        if rec is not None:
+            print(json.dumps(rec), flush=True)
+    finally:
+        if dist is not None:
+            dist.destroy_process_group()
+    return 0 if verified else 1
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -855,6 +855,16 @@ static void *bench_worker(void *arg) {
     else
 #endif
       apply_scalar(nin, J->nout, J->tbl, in, out, bs);
+    /* decode in place: a rebuilt block staged in the tail buffer goes back
+     * into the object (its valid bytes) */
+    if (J->op != 0)
+      for (int i = 0; i < J->nout; i++) {
+        uint64_t b = (uint64_t)J->want[i];
+        if (b >= filled && b * bs < J->size) {
+          uint64_t n = J->size - b * bs < bs ? J->size - b * bs : bs;
+          memcpy((uint8_t *)obj + b * bs, out[i], n);
+        }
+      }
   }
   free(tail);
   free(dec);
@@ -869,19 +879,26 @@ int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride
   uint32_t *C = malloc(sizeof(uint32_t) * m * k);
   uint32_t *rows = malloc(sizeof(uint32_t) * (m + k) * k);
   uint8_t *tbl = malloc((size_t)(m + k) * k * 32);
-  int surv[256], nout;
+  int surv[256], want[256], nout;
   int rc = orc_vandermonde_coding_matrix(k, m, 8, C);
   if (rc) goto done;
   if (op == 0) {
     nout = m;
     memcpy(rows, C, sizeof(uint32_t) * m * k);
   } else {
+    /* erased ids may include coding blocks: they are only excluded from the
+     * survivors; the rebuilt (wanted) blocks are the erased data blocks */
     int er[256] = {0};
-    for (int i = 0; i < nerased; i++) er[erased[i]] = 1;
+    for (int i = 0; i < nerased; i++) {
+      if (erased[i] < 0 || erased[i] >= k + m) { rc = ORC_E_PARAMS; goto done; }
+      er[erased[i]] = 1;
+    }
     int j = 0;
     for (int i = 0; i < k + m && j < k; i++) if (!er[i]) surv[j++] = i;
-    nout = nerased;
-    rc = decode_map_gf(ORC_VANDRS, k, m, 8, C, surv, erased, nerased, rows);
+    if (j < k) { rc = ORC_E_PARAMS; goto done; }
+    nout = 0;
+    for (int i = 0; i < k; i++) if (er[i]) want[nout++] = i;
+    rc = decode_map_gf(ORC_VANDRS, k, m, 8, C, surv, want, nout, rows);
     if (rc) goto done;
   }
   init_tables(nout, k, rows, tbl);
@@ -899,7 +916,7 @@ int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride
       J->objs = objs; J->stride = obj_stride; J->size = size; J->bs = bs;
       J->o0 = (int)((long long)nobj * t / threads);
       J->o1 = (int)((long long)nobj * (t + 1) / threads);
-      J->parity = parity; J->tbl = tbl; J->mats = mats; J->want = erased; J->surv = surv;
+      J->parity = parity; J->tbl = tbl; J->mats = mats; J->want = want; J->surv = surv;
       pthread_create(&th[t], NULL, bench_worker, J);
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);

@@ -1,12 +1,75 @@
-"""Multi-process path of bench.py on CPU: world_size-2 gloo ranks shard the
-object batch with no data-path collective, and the timing uses a barrier and
-a max-reduce, as the MI355X run does over RCCL."""
+"""bench.py's own rank logic on CPU (bench.main -> run_rank), with the device
+calls stubbed by the CPU oracle: world_size-2 gloo ranks shard the objects
+with no data-path collective, time with a barrier + max over ranks, and the
+line's `verified` flag fails for a decode that writes nothing."""
+import contextlib
+import io
+import json
 import os
 import socket
+import sys
+import time
 
 import pytest
-import torch.distributed as dist
+import torch
 import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+class CpuEvent:
+    def record(self, stream=None):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1e3
+
+
+class CpuBackend:
+    """bench.GpuBackend's interface over host tensors; encode/decode are the
+    oracle's batch driver (the same ops the GPU runs)."""
+
+    def __init__(self, local_rank, world, oversubscribe=False):
+        self.name = f"cpu-stub:{local_rank}"
+
+    def random_batch(self, n, size, seed):
+        g = torch.Generator().manual_seed(seed)
+        return torch.randint(0, 256, (n, size), dtype=torch.uint8, generator=g)
+
+    def empty(self, n, cols):
+        return torch.empty((n, cols), dtype=torch.uint8)
+
+    def encode(self, objs, size, parity):
+        from oracle import oracle as O
+        O.bench_rs8(0, bench.K, bench.M, objs.numpy(), objs.stride(0), size, objs.shape[0],
+                    parity.numpy(), threads=1)
+
+    def decode(self, objs, size, parity, erased):
+        from oracle import oracle as O
+        O.bench_rs8(1, bench.K, bench.M, objs.numpy(), objs.stride(0), size, objs.shape[0],
+                    parity.numpy(), erased=erased, threads=1)
+
+    def sync(self):
+        pass
+
+    def event(self):
+        return CpuEvent()
+
+
+class NoopDecode(CpuBackend):
+    def decode(self, objs, size, parity, erased):
+        pass
+
+
+class ZeroEncode(CpuBackend):
+    def encode(self, objs, size, parity):
+        parity.zero_()
+
+
+BACKENDS = {"cpu": CpuBackend, "noop_decode": NoopDecode, "zero_encode": ZeroEncode}
 
 
 def _free_port():
@@ -17,44 +80,116 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, total, q):
-    import sys
-    import time
-
-    import torch
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    import bench
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    lo, hi = bench.shard_range(rank, world, total)
-    dist.barrier()
-    t0 = time.perf_counter()
-    time.sleep(0.05 * (rank + 1))   # ranks finish at different times
-    dist.barrier()
-    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    cover = torch.zeros(total, dtype=torch.int32)
-    cover[lo:hi] += 1
-    dist.all_reduce(cover)   # test-only check that shards tile the batch
-    q.put((rank, lo, hi, elapsed.item(), cover.tolist()))
-    dist.destroy_process_group()
+def _worker(rank, world, port, argv, backend, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      LOCAL_RANK=str(rank), WORLD_SIZE=str(world))
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        rc = bench.main(argv, backend=BACKENDS[backend])
+    q.put((rank, rc, out.getvalue()))
 
 
-@pytest.mark.parametrize("world,total", [(2, 1024), (2, 7)])
-def test_gloo_two_ranks_shard_and_time(world, total):
+def _run_ranks(world, argv, backend="cpu"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, total, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, argv, backend, q))
+             for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=120) for _ in procs)
+    res = sorted(q.get(timeout=180) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    spans = [(lo, hi) for _, lo, hi, _, _ in res]
+    return res
+
+
+SMALL = ["--steps", "3", "--warmup", "1", "--warmup-s", "0", "--size", "65536"]
+
+
+def test_two_ranks_weak_scaling_through_bench_main():
+    res = _run_ranks(2, ["--gpus", "2", "--objects", "5"] + SMALL)
+    (r0, rc0, out0), (r1, rc1, out1) = res
+    assert rc0 == 0 and rc1 == 0
+    assert out1 == ""                       # one line, from rank 0
+    rec = json.loads(out0)
+    assert rec["n_gpus"] == 2 and rec["scaling"] == "weak" and rec["verified"] is True
+    assert [r["objects"] for r in rec["per_rank"]] == [[0, 5], [5, 10]]
+    assert rec["config"]["global_objects"] == 10
+    assert rec["cpu_baseline"] is None      # rank 0 at N=1 only
+    # value = all ranks' objects / the slowest rank's time
+    el = max(r["elapsed_s"] for r in rec["per_rank"])
+    assert rec["value"] == pytest.approx(2 * 10 * 65536 * 3 / el / 2**30, rel=2e-2)
+    assert all(all(r["checks"].values()) for r in rec["per_rank"])
+
+
+def test_two_ranks_partitioned_batch():
+    """configs[4]: one global batch split with shard_range (strong scaling)."""
+    res = _run_ranks(2, ["--gpus", "2", "--workload", "64MiB", "--objects", "7"] + SMALL)
+    rec = json.loads(res[0][2])
+    assert rec["scaling"] == "strong" and rec["verified"] is True
+    assert [r["objects"] for r in rec["per_rank"]] == [[0, 3], [3, 7]]
+    assert rec["config"]["global_objects"] == 7
+
+
+def test_noop_decode_fails_verification_on_a_rank():
+    res = _run_ranks(2, ["--gpus", "2", "--objects", "3"] + SMALL, backend="noop_decode")
+    rec = json.loads(res[0][2])
+    assert rec["verified"] is False
+    assert res[0][1] == 1 and res[1][1] == 1
+    assert not rec["per_rank"][1]["checks"]["poisoned_decode_0_1_2_3"]
+
+
+def test_single_rank_cpu_leg_checks_parity(monkeypatch):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    argv = ["--objects", "4", "--cpu-seconds", "0.05", "--cpu-objects", "3"] + SMALL
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        rc = bench.main(argv, backend=CpuBackend)
+    rec = json.loads(out.getvalue())
+    assert rc == 0 and rec["verified"] is True and rec["n_gpus"] == 1
+    cb = rec["cpu_baseline"]
+    assert cb["parity_vs_gpu"] == {"objects": 3, "equal": True}
+    assert cb["cores"] >= 1 and cb["host_cpus"] >= cb["cores"] and cb["affinity_cpus"] >= 1
+
+
+def test_single_rank_wrong_parity_fails(monkeypatch):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    argv = ["--objects", "3", "--cpu-seconds", "0.01", "--cpu-objects", "2"] + SMALL
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        rc = bench.main(argv, backend=ZeroEncode)
+    rec = json.loads(out.getvalue())
+    assert rc == 1 and rec["verified"] is False
+    assert rec["cpu_baseline"]["parity_vs_gpu"]["equal"] is False
+
+
+def test_gpus_flag_launches_ranks(monkeypatch):
+    """--gpus N without a launcher starts N ranks in a child process (before
+    any GPU call) and returns its status."""
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    seen = {}
+
+    def fake_call(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return 7
+
+    monkeypatch.setattr(bench.subprocess, "call", fake_call)
+    assert bench.main(["--gpus", "4", "--steps", "5"]) == 7
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
+    assert cmd[-3:] == ["--gpus", "4", "--steps", "5"][-3:]
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_gpus_must_match_world(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert bench.main(["--gpus", "4"], backend=CpuBackend) == 2
+
+
+@pytest.mark.parametrize("world,total", [(2, 1024), (2, 7), (8, 64), (3, 2)])
+def test_shard_range_tiles_the_batch(world, total):
+    spans = [bench.shard_range(r, world, total) for r in range(world)]
     assert spans[0][0] == 0 and spans[-1][1] == total
     assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
-    assert all(c == 1 for c in res[0][4])
-    # max over ranks: everyone reports the slowest rank's time
-    assert res[0][3] == res[1][3] and res[0][3] >= 0.1

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
-STEPS=${STEPS:-smoke,test,bench,prof}
+STEPS=${STEPS:-smoke,test,bench1,prof}
 
 fatal() {  # exit codes that mean the GPU step crashed or hung
   case "$1" in 124|134|137|139|143) return 0;; esac
@@ -27,8 +27,10 @@ run() {  # name timeout cmd...
 }
 
 [[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-[[ $STEPS == *test* ]] && run pytest 1200 python -m pytest tests -x -q -m gpu ${PYTEST_ARGS:-}
-[[ $STEPS == *bench* ]] && run bench 600 python bench.py ${BENCH_ARGS:-}
+[[ $STEPS == *test* ]] && run pytest 1200 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}
+[[ $STEPS == *bench1* ]] && run bench 600 python bench.py ${BENCH_ARGS:-}
+[[ $STEPS == *bench2* ]] && run bench2 600 python bench.py --gpus 2 --oversubscribe --steps 50 --warmup 10
+[[ $STEPS == *bench64* ]] && run bench64 600 python bench.py --workload 64MiB --steps 50 --warmup 10 --no-cpu
 if [[ $STEPS == *prof* ]]; then
   cd /tmp && export TMPDIR=/tmp
   run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- \
