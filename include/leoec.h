@@ -29,6 +29,10 @@
 extern "C" {
 #endif
 
+/* The library is built with hidden visibility; everything declared here is
+ * its export table. */
+#pragma GCC visibility push(default)
+
 /* Coding classes — same numbering as CodingType (c_src/leo_erasure_nif.cpp:36-42);
  * atom names vandrs | cauchyrs | liberation | isars (nif.cpp:61-72). */
 enum leoec_coding {
@@ -105,7 +109,11 @@ int leoec_repair(int coding, int k, int m, int w, const uint8_t *const *blocks, 
  * All pointers are HIP device pointers, 16-byte aligned, strides multiples
  * of 16; work is enqueued on `stream` (a hipStream_t, NULL = default stream)
  * and the call returns without synchronising.  `nobj` objects are processed
- * per call; object o's block j lives at base + o*stride + j*block_size.   */
+ * per call; object o's block j lives at base + o*stride + j*block_size.
+ * Strides cover a whole row (obj_stride >= size, parity_stride >=
+ * m*block_size, block/out strides >= block_size) for every nobj >= 1;
+ * otherwise LEOEC_E_ARG.  The buffers themselves cannot be checked here:
+ * they must hold nobj rows.                                                */
 
 /* Encode nobj objects of `size` bytes each, stored at objs + o*obj_stride
  * (the unpadded object; bytes past `size` inside the last data block are
@@ -143,6 +151,8 @@ int leoec_device(void);
 
 /* Library version string. */
 const char *leoec_version(void);
+
+#pragma GCC visibility pop
 
 #ifdef __cplusplus
 }

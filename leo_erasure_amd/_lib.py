@@ -15,6 +15,10 @@ except Exception:  # pragma: no cover - torch is optional for the host API
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libleoec.so")
+# The measurement build (every A/B kernel form, LEOEC_* knobs read once at
+# first use): `make -C leo_erasure_amd/csrc measure`.  Tools select it with
+# LEOEC_LIBRARY=measure; the form-parity tests switch to it with use_library().
+MEASURE_LIB_PATH = os.path.join(_HERE, "libleoec_measure.so")
 
 CAUCHYRS, VANDRS, LIBERATION, ISARS = 1, 2, 3, 4
 CODING_IDS = {"cauchyrs": CAUCHYRS, "vandrs": VANDRS, "liberation": LIBERATION, "isars": ISARS}
@@ -41,12 +45,17 @@ class LeoecError(Exception):
         super().__init__(strerror(code))
 
 
-def _load():
-    if not os.path.exists(LIB_PATH):
+_loaded = {}
+
+
+def _load(path=LIB_PATH):
+    if path in _loaded:
+        return _loaded[path]
+    if not os.path.exists(path):
         raise ImportError(
-            f"{LIB_PATH} is missing: build the HIP engine first "
+            f"{path} is missing: build the HIP engine first "
             "(python -c 'import __graft_entry__ as g; g.build()' or make -C leo_erasure_amd/csrc)")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     c_int, u64 = ctypes.c_int, ctypes.c_uint64
     vp, u8p = ctypes.c_void_p, ctypes.c_void_p
     L.leoec_strerror.restype = ctypes.c_char_p
@@ -69,10 +78,49 @@ def _load():
                                                  u64, vp]
     L.leoec_coding_matrix.argtypes = [c_int] * 4 + [ctypes.POINTER(ctypes.c_uint32), c_int,
                                                     ctypes.POINTER(c_int)]
+    if hasattr(L, "leoec_measure_reload"):
+        L.leoec_measure_reload.argtypes = []
+        L.leoec_measure_reload.restype = None
+    _loaded[path] = L
     return L
 
 
-lib = _load()
+_current = _load(MEASURE_LIB_PATH if os.environ.get("LEOEC_LIBRARY") == "measure" else LIB_PATH)
+
+
+class _LibProxy:
+    """`lib.leoec_*` resolves against the library in use (use_library)."""
+    __slots__ = ()
+
+    def __getattr__(self, name):
+        return getattr(_current, name)
+
+
+lib = _LibProxy()
+
+
+def library_path():
+    return _current._name
+
+
+def use_library(path):
+    """Route every later call through the library at `path`; returns the
+    previous library's path."""
+    global _current
+    prev = _current._name
+    _current = _load(path)
+    return prev
+
+
+def is_measure_build():
+    return hasattr(_current, "leoec_measure_reload")
+
+
+def measure_reload():
+    """Measurement build only: re-read the LEOEC_* knobs from the environment."""
+    if not is_measure_build():
+        raise RuntimeError(f"{library_path()} is the product build: it has no LEOEC_* knobs")
+    _current.leoec_measure_reload()
 
 
 def strerror(code):

@@ -16,6 +16,7 @@
 #include <tuple>
 
 #include "../../include/leoec.h"
+#include "knobs.hpp"
 
 namespace leoec {
 
@@ -250,15 +251,6 @@ int lib_dec_plan(const Code& c, const int* surv, const std::vector<Shard>& in, c
   return LEOEC_OK;
 }
 
-namespace {
-// LEOEC_BITMATRIX=1 forces the generic masked-bitmatrix kernel for cauchyrs
-// (measurement / cross-check of the bitsliced GF path).
-int bitmatrix_env() {
-  const char* e = std::getenv("LEOEC_BITMATRIX");
-  return e ? std::atoi(e) : 0;
-}
-}  // namespace
-
 int apply(const Code& c, const int* surv, const std::vector<Shard>& in, const int* want,
           const std::vector<Shard>& out, uint64_t bs, uint64_t nobj, hipStream_t s) {
   const int nwant = (int)out.size();
@@ -276,7 +268,7 @@ int apply(const Code& c, const int* surv, const std::vector<Shard>& in, const in
     p.nobj = nobj;
     return launch(p, s);
   }
-  if (c.coding == LEOEC_CAUCHYRS && gfbit_supported(c.w) && bitmatrix_env() == 0) {
+  if (c.coding == LEOEC_CAUCHYRS && gfbit_supported(c.w) && knobs().bitmatrix == 0) {
     // cauchyrs bitmatrices (coding and decoding) are bit expansions of GF(2^w)
     // matrices: apply the GF map on the packet-bitsliced blocks directly
     GfBitApply p;
@@ -409,12 +401,12 @@ thread_local Staging tl_staging;  // one stream + device buffer per calling thre
 enum class StageForm { kAuto, kPageable, kGather, kRing };
 
 StageForm stage_form() {
-  const char* e = std::getenv("LEOEC_HOST_STAGING");
-  if (!e) return StageForm::kAuto;
-  if (std::strcmp(e, "pinned") == 0) return StageForm::kRing;
-  if (std::strcmp(e, "gather") == 0) return StageForm::kGather;
-  if (std::strcmp(e, "pageable") == 0) return StageForm::kPageable;
-  return StageForm::kAuto;
+  switch (knobs().host_staging) {  // LEOEC_HOST_STAGING (measurement build)
+    case 1: return StageForm::kPageable;
+    case 2: return StageForm::kGather;
+    case 3: return StageForm::kRing;
+    default: return StageForm::kAuto;
+  }
 }
 
 bool gather_wanted(size_t nsegs) {
@@ -450,8 +442,7 @@ uint8_t* gather_buf(Staging* st, size_t bytes) {
 }
 
 size_t stage_chunk_bytes() {
-  const char* e = std::getenv("LEOEC_STAGE_CHUNK_KIB");
-  long v = e ? std::atol(e) : 256;
+  long v = knobs().stage_chunk_kib;
   if (v < 16) v = 16;
   if (v > 8192) v = 8192;
   return (size_t)v << 10;
@@ -841,7 +832,7 @@ int op_encode_dev(int coding, int k, int m, int w, const uint8_t* objs, uint64_t
   if (rc) return rc;
   if (nobj == 0 || bs == 0) return LEOEC_OK;
   if (!objs || !parity) return LEOEC_E_ARG;
-  if ((nobj > 1 && (obj_stride < size || parity_stride < (uint64_t)m * bs))) return LEOEC_E_ARG;
+  if (obj_stride < size || parity_stride < (uint64_t)m * bs) return LEOEC_E_ARG;
   if ((rc = device_init())) return rc;
   const Code* c;
   if ((rc = get_code(coding, k, m, w, &c))) return rc;
@@ -878,6 +869,7 @@ int op_decode_dev(int coding, int k, int m, int w, uint8_t* objs, uint64_t obj_s
     if (gone[id] && (uint64_t)id * bs < size) want.push_back(id);
   if (want.empty() || nobj == 0 || bs == 0) return LEOEC_OK;
   if (!objs || !parity) return LEOEC_E_ARG;
+  if (obj_stride < size || parity_stride < (uint64_t)m * bs) return LEOEC_E_ARG;
   if ((rc = device_init())) return rc;
   const Code* c;
   if ((rc = get_code(coding, k, m, w, &c))) return rc;
@@ -911,6 +903,7 @@ int op_repair_dev(int coding, int k, int m, int w, const uint8_t* const* blocks,
     if (!out[r]) return LEOEC_E_ARG;
   }
   if (nrep == 0 || nobj == 0 || bs == 0) return LEOEC_OK;
+  if (block_stride < bs || out_stride < bs) return LEOEC_E_ARG;
   if ((rc = device_init())) return rc;
   const Code* c;
   if ((rc = get_code(coding, k, m, w, &c))) return rc;

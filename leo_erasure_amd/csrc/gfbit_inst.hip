@@ -1,10 +1,10 @@
 // gfbit_inst.hip — launches of the packet-bitsliced GF(2^w) kernel
 // (kernels_impl.hpp gfbit_apply) for w = 2..16, R <= 4 outputs per launch,
 // inputs beyond 16 folded in by accumulating launches.
-#include <cstdlib>
 #include <utility>
 
 #include "kernels_impl.hpp"
+#include "knobs.hpp"
 
 namespace leoec {
 
@@ -32,9 +32,8 @@ int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint6
       a.coef[i][j] = j < nk ? p.coef[(size_t)(r0 + i) * p.K + j0 + j] : 0u;
   }
   // objects interleaved over the XCDs (xcd_obj_map) for objects of at most
-  // kObjMapMaxTiles tiles; LEOEC_GFBIT_XMAP=0 turns it off (A/B)
-  const char* xe = std::getenv("LEOEC_GFBIT_XMAP");
-  a.xmap = (XMAP == 0 && a.tiles <= kObjMapMaxTiles && !(xe && std::atoi(xe) == 0)) ? 1u : 0u;
+  // kObjMapMaxTiles tiles; Knobs::gfbit_xmap = 0 turns it off (A/B)
+  a.xmap = (XMAP == 0 && a.tiles <= kObjMapMaxTiles && knobs().gfbit_xmap != 0) ? 1u : 0u;
   if (KR > 0 && nk > KR) return LEOEC_E_ARG;
   hipLaunchKernelGGL((gfbit_apply<W, R, LW, ACC, PF, CEIL, KR, WG, XMAP>),
                      dim3((uint32_t)(no * a.tiles)), dim3(WG), 0, s, a);
@@ -43,6 +42,7 @@ int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint6
 
 constexpr int kPF = 1;  // blocks of load look-ahead (kernels_impl.hpp gfbit_apply)
 
+#ifdef LEOEC_MEASURE
 template <int W, int R, bool ACC>
 int launch_gfb_lds_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
                      hipStream_t s) {
@@ -62,6 +62,7 @@ int launch_gfb_lds_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, u
                      dim3(kGfbLdsThreads), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }
+#endif  // LEOEC_MEASURE
 
 template <int W, int LW, int PF = kPF>
 GfbFn pick_r(int r, bool acc) {
@@ -73,21 +74,11 @@ GfbFn pick_r(int r, bool acc) {
   return tbl[acc ? 1 : 0][r - 1];
 }
 
-// LEOEC_GFBIT_LW=1|2|4 selects the lane width (dwords per packet per lane)
-// for w = 8 measurements; the shipped width is 2.
-int lane_width_env() {
-  const char* e = std::getenv("LEOEC_GFBIT_LW");
-  return e ? std::atoi(e) : 2;
-}
-
-// LEOEC_GFBIT_PF=0|1|2|3 sets the load look-ahead (blocks) for w = 8
-// measurements.
-int prefetch_env() {
-  const char* e = std::getenv("LEOEC_GFBIT_PF");
-  return e ? std::atoi(e) : kPF;
-}
-
-// LEOEC_GFBIT_WG=64 (measurement): 64-lane workgroups (512-B tiles per packet)
+#ifdef LEOEC_MEASURE
+// Measurement forms of the w = 8 kernel (Knobs::gfbit_*): lane width
+// (dwords per packet per lane, shipped 2), load look-ahead (blocks, shipped
+// 1), 64-lane workgroups, the traffic-ceiling kernel (not a code),
+// object-contiguous XCD map, LDS-staged inputs.
 template <int W, int LW>
 GfbFn pick_r_wg64(int r, bool acc) {
   static const GfbFn tbl[2][kMaxR] = {
@@ -98,49 +89,48 @@ GfbFn pick_r_wg64(int r, bool acc) {
   return tbl[acc ? 1 : 0][r - 1];
 }
 
-GfbFn pick(int w, int r, bool acc, int nk) {
-  if (w == 8) {
-    if (const char* wg = std::getenv("LEOEC_GFBIT_WG"))
-      if (std::atoi(wg) == 64) return pick_r_wg64<8, 2>(r, acc);
-    const int lw = lane_width_env();
-    const char* ce = std::getenv("LEOEC_GFBIT_CEIL");  // measurement only: not a code
-    if (ce && std::atoi(ce) && r == 4 && !acc) return &launch_gfb_t<8, 4, 2, false, kPF, true>;
-    // LEOEC_GFBIT_XMAP (measurement): 0 = workgroup ids in dispatch order,
-    // 1 = all tiles of an object on one XCD, contiguous object ranges per XCD;
-    // default: objects interleaved over the XCDs (xcd_obj_map) when an
-    // object has at most kObjMapMaxTiles tiles (launch_gfb_t)
-    if (const char* xm = std::getenv("LEOEC_GFBIT_XMAP"))
-      if (std::atoi(xm) == 1 && r == 4 && !acc) return &launch_gfb_t<8, 4, 2, false, kPF, false, 0, kThreads, 1>;
-    // LEOEC_GFBIT_LDS=1 (measurement): LDS-staged inputs
-    if (const char* le = std::getenv("LEOEC_GFBIT_LDS")) {
-      if (std::atoi(le) == 1) {
-        static const GfbFn tbl[2][kMaxR] = {
-            {&launch_gfb_lds_t<8, 1, false>, &launch_gfb_lds_t<8, 2, false>,
-             &launch_gfb_lds_t<8, 3, false>, &launch_gfb_lds_t<8, 4, false>},
-            {&launch_gfb_lds_t<8, 1, true>, &launch_gfb_lds_t<8, 2, true>,
-             &launch_gfb_lds_t<8, 3, true>, &launch_gfb_lds_t<8, 4, true>}};
-        return tbl[acc ? 1 : 0][r - 1];
-      }
-    }
-    const int pf = prefetch_env();
-    if (pf == 0) {
-      if (lw == 1) return pick_r<8, 1, 0>(r, acc);
-      if (lw == 4) return pick_r<8, 4, 0>(r, acc);
-      return pick_r<8, 2, 0>(r, acc);
-    }
-    if (pf == 2) {
-      if (lw == 1) return pick_r<8, 1, 2>(r, acc);
-      return pick_r<8, 2, 2>(r, acc);
-    }
-    if (pf == 3) {
-      if (lw == 1) return pick_r<8, 1, 3>(r, acc);
-      return pick_r<8, 2, 3>(r, acc);
-    }
-    if (lw == 1) return pick_r<8, 1>(r, acc);
-    if (lw == 4) return pick_r<8, 4>(r, acc);
-    return pick_r<8, 2>(r, acc);
+GfbFn pick_measure8(int r, bool acc) {
+  const Knobs& kn = knobs();
+  if (kn.gfbit_wg == 64) return pick_r_wg64<8, 2>(r, acc);
+  const int lw = kn.gfbit_lw;
+  if (kn.gfbit_ceil && r == 4 && !acc) return &launch_gfb_t<8, 4, 2, false, kPF, true>;
+  if (kn.gfbit_xmap == 1 && r == 4 && !acc)
+    return &launch_gfb_t<8, 4, 2, false, kPF, false, 0, kThreads, 1>;
+  if (kn.gfbit_lds == 1) {
+    static const GfbFn tbl[2][kMaxR] = {
+        {&launch_gfb_lds_t<8, 1, false>, &launch_gfb_lds_t<8, 2, false>,
+         &launch_gfb_lds_t<8, 3, false>, &launch_gfb_lds_t<8, 4, false>},
+        {&launch_gfb_lds_t<8, 1, true>, &launch_gfb_lds_t<8, 2, true>,
+         &launch_gfb_lds_t<8, 3, true>, &launch_gfb_lds_t<8, 4, true>}};
+    return tbl[acc ? 1 : 0][r - 1];
   }
+  const int pf = kn.gfbit_pf;
+  if (pf == 0) {
+    if (lw == 1) return pick_r<8, 1, 0>(r, acc);
+    if (lw == 4) return pick_r<8, 4, 0>(r, acc);
+    return pick_r<8, 2, 0>(r, acc);
+  }
+  if (pf == 2) {
+    if (lw == 1) return pick_r<8, 1, 2>(r, acc);
+    return pick_r<8, 2, 2>(r, acc);
+  }
+  if (pf == 3) {
+    if (lw == 1) return pick_r<8, 1, 3>(r, acc);
+    return pick_r<8, 2, 3>(r, acc);
+  }
+  if (lw == 1) return pick_r<8, 1>(r, acc);
+  if (lw == 4) return pick_r<8, 4>(r, acc);
+  return pick_r<8, 2>(r, acc);
+}
+#endif  // LEOEC_MEASURE
+
+GfbFn pick(int w, int r, bool acc, int nk) {
+  (void)nk;
+#ifdef LEOEC_MEASURE
+  if (w == 8) return pick_measure8(r, acc);
+#endif
   switch (w) {
+    case 8: return pick_r<8, 2>(r, acc);
     case 2: return pick_r<2, 2>(r, acc);
     case 3: return pick_r<3, 2>(r, acc);
     case 4: return pick_r<4, 2>(r, acc);

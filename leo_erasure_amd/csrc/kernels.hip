@@ -1,10 +1,10 @@
 // kernels.hip — dispatch of GfApply / BitApply plans onto the gfx950 kernels
 // of kernels_impl.hpp (w = 16/32 and bitmatrix instances live here; GF(2^8)
 // instances in gf8_inst.hip).
-#include <cstdlib>
 #include <utility>
 
 #include "kernels_impl.hpp"
+#include "knobs.hpp"
 
 namespace leoec {
 
@@ -24,6 +24,7 @@ ChunkFn gf8_pick(std::index_sequence<I...>, int k, int r, bool acc) {
   return sel[k - 1](r, acc);
 }
 
+#ifdef LEOEC_MEASURE
 ChunkFn gf16_pick(int r, bool acc) {
   static const ChunkFn tbl[2][kMaxR] = {
       {&launch_gf16_t<1, false>, &launch_gf16_t<2, false>, &launch_gf16_t<3, false>,
@@ -33,18 +34,24 @@ ChunkFn gf16_pick(int r, bool acc) {
   return tbl[acc ? 1 : 0][r - 1];
 }
 
-// LEOEC_GFW_FORM selects the w = 16 / 32 kernel (A/B measurements):
+#endif  // LEOEC_MEASURE
+
+// Knobs::gfw_form selects the w = 16 / 32 kernel (measurement build):
 //   0 byte-plane v_perm (gfp_apply, shipped)
 //   1 w=16: 2-bit-field v_perm (gf16_apply); w=32: shift-and-add
 //   2 shift-and-add (gfw_apply)
-// LEOEC_GFP_CPT=1|2 sets gfp_apply's 16-byte columns per lane.
-int env_int(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
-
+// Knobs::gfp_cpt = 1|2 sets gfp_apply's 16-byte columns per lane (2 shipped).
 template <int W>
 ChunkFn gfp_pick(int r, bool acc, int cpt) {
+#ifndef LEOEC_MEASURE
+  (void)cpt;
+  static const ChunkFn tbl[2][kMaxR] = {
+      {&launch_gfp_t<W, 1, false, 2>, &launch_gfp_t<W, 2, false, 2>, &launch_gfp_t<W, 3, false, 2>,
+       &launch_gfp_t<W, 4, false, 2>},
+      {&launch_gfp_t<W, 1, true, 2>, &launch_gfp_t<W, 2, true, 2>, &launch_gfp_t<W, 3, true, 2>,
+       &launch_gfp_t<W, 4, true, 2>}};
+  return tbl[acc ? 1 : 0][r - 1];
+#else
   static const ChunkFn tbl[2][2][kMaxR] = {
       {{&launch_gfp_t<W, 1, false, 1>, &launch_gfp_t<W, 2, false, 1>,
         &launch_gfp_t<W, 3, false, 1>, &launch_gfp_t<W, 4, false, 1>},
@@ -55,7 +62,10 @@ ChunkFn gfp_pick(int r, bool acc, int cpt) {
        {&launch_gfp_t<W, 1, true, 2>, &launch_gfp_t<W, 2, true, 2>, &launch_gfp_t<W, 3, true, 2>,
         &launch_gfp_t<W, 4, true, 2>}}};
   return tbl[cpt == 2 ? 1 : 0][acc ? 1 : 0][r - 1];
+#endif
 }
+
+#ifdef LEOEC_MEASURE
 
 template <int W>
 ChunkFn gfw_pick(int r, bool acc) {
@@ -67,9 +77,11 @@ ChunkFn gfw_pick(int r, bool acc) {
   return tbl[acc ? 1 : 0][r - 1];
 }
 
-// LEOEC_GF8_VARIANT=<n> selects a measurement variant of gf8_apply<10,4>
-// (tools/kvariants.py); unset or 0 = the shipped kernel.
-// LEOEC_BIT_FORM selects the bitmatrix kernel form for measurements:
+#endif  // LEOEC_MEASURE
+
+// Knobs::gf8_variant = <n> selects a measurement variant of gf8_apply<10,4>
+// (tools/kvariants.py); 0 = the shipped kernel.
+// Knobs::bit_form selects the bitmatrix kernel form for measurements:
 //   0 masked, no look-ahead        1 masked, 1 packet ahead
 //   2 branchy, no look-ahead       3 branchy, 1 packet ahead
 //   4/5/6 masked, 2/3/5 packets ahead (4 = shipped)
@@ -78,14 +90,9 @@ ChunkFn gfw_pick(int r, bool acc) {
 //   9 as 4, objects interleaved over the XCDs (xcd_obj_map)
 // Measured on liberation(7,2,7): masked beats branchy (the scalar branches
 // cost more than the masked xors they save); look-ahead depth see DESIGN.md.
-int bit_form_env() {
-  const char* e = std::getenv("LEOEC_BIT_FORM");
-  const int f = e ? std::atoi(e) : 4;
-  return (f >= 0 && f <= 9) ? f : 4;
-}
-
 using BitFn = void (*)(const detail::BitArgs);
 
+#ifdef LEOEC_MEASURE
 template <int RO, bool ACC>
 BitFn bit_kernel_f(int form) {
   switch (form) {
@@ -106,6 +113,7 @@ BitFn bit_kernel(int ro, bool acc, int form) {
   if (ro == 16) return acc ? bit_kernel_f<16, true>(form) : bit_kernel_f<16, false>(form);
   return acc ? bit_kernel_f<32, true>(form) : bit_kernel_f<32, false>(form);
 }
+#endif  // LEOEC_MEASURE
 
 // Shipped form with the output-packet count rounded up to even only (2..32):
 // liberation(k,2,w) has 2w output packets (14 at w=7, 22 at w=11), which the
@@ -116,11 +124,6 @@ BitFn bit_kernel_even(std::index_sequence<I...>, int rp, bool acc) {
       {&detail::bit_apply<2 * ((int)I + 1), false, false, 2>...},
       {&detail::bit_apply<2 * ((int)I + 1), true, false, 2>...}};
   return tbl[acc ? 1 : 0][(rp + 1) / 2 - 1];
-}
-
-int gf8_variant_env() {
-  const char* e = std::getenv("LEOEC_GF8_VARIANT");
-  return e ? std::atoi(e) : 0;
 }
 
 // True when the plan is exactly a liberation encode bitmatrix (the structure
@@ -143,25 +146,27 @@ bool is_liberation_encode(const BitApply& p) {
   return true;
 }
 
-// LEOEC_LIB_FORM=0 routes liberation encodes through the generic masked
-// bitmatrix kernel (A/B and parity of both forms); default 1 = lib_apply.
-// LEOEC_LIB_LA=2|4|8 sets lib_apply's packet look-ahead (A/B; default 2:
-// profiles/r01_v13_ab_lib_la.log, best or within 1 % of best for w = 5..13).
+// Knobs::lib_form = 0 routes liberation encodes through the generic masked
+// bitmatrix kernel (A/B and parity of both forms); 1 = lib_apply (shipped).
+// Knobs::lib_la = 2|4|8 sets lib_apply's packet look-ahead (measurement
+// build; shipped 2: profiles/r01_v13_ab_lib_la.log, best or within 1 % of
+// best for w = 5..13).
 using LibFn = void (*)(const detail::LibArgs);
 template <int W>
 LibFn lib_kernel_w(int la) {
+#ifdef LEOEC_MEASURE
   if (la == 4) return &detail::lib_apply<W, 4>;
   if (la == 8) return &detail::lib_apply<W, 8>;
+#endif
+  (void)la;
   return &detail::lib_apply<W, 2>;
 }
-// LEOEC_LIB_XMAP=0 (A/B): workgroup ids in dispatch order instead of the
+// Knobs::lib_xmap = 0 (A/B): workgroup ids in dispatch order instead of the
 // object-interleaved XCD map (xcd_obj_map, kernels_impl.hpp) that the
 // launchers use for objects of at most kObjMapMaxTiles tiles
-bool obj_map(uint32_t tiles, const char* env) {
-  return tiles <= kObjMapMaxTiles && env_int(env, 2) != 0;
-}
+bool obj_map(uint32_t tiles) { return tiles <= kObjMapMaxTiles && knobs().lib_xmap != 0; }
 LibFn lib_kernel(int w) {
-  const int la = env_int("LEOEC_LIB_LA", 2);
+  const int la = knobs().lib_la;
   switch (w) {
     case 3: return lib_kernel_w<3>(la);
     case 5: return lib_kernel_w<5>(la);
@@ -182,7 +187,7 @@ int launch_lib(const BitApply& p, LibFn fn, hipStream_t s) {
     a.k = p.KB;
     a.ps = ps;
     a.tiles = tiles;
-    a.xmap = obj_map(tiles, "LEOEC_LIB_XMAP") ? 1u : 0u;
+    a.xmap = obj_map(tiles) ? 1u : 0u;
     uint32_t vmin = 0xFFFFFFFFu;
     for (int j = 0; j < kMaxK; ++j) {
       a.in[j] = j < p.KB ? dev_shard(p.in[j], o0) : DevShard{nullptr, 0, 0, 0};
@@ -212,11 +217,11 @@ int device_cus() {
   }();
   return cus;
 }
-int gfp_blocks_per_cu() { return env_int("LEOEC_GFP_BPC", 64); }
-// LEOEC_GF8_TMAP: gf8_apply workgroup -> tile order (Gf8Args::tmap), A/B only.
-int gf8_tile_map() { return env_int("LEOEC_GF8_TMAP", 0); }
-int gf8_wg_env() { return env_int("LEOEC_GF8_WG", 0); }
-bool gf8_tile_map_set() { return std::getenv("LEOEC_GF8_TMAP") != nullptr; }
+int gfp_blocks_per_cu() { return knobs().gfp_bpc; }
+// Knobs::gf8_tmap: gf8_apply workgroup -> tile order (Gf8Args::tmap), A/B only.
+int gf8_tile_map() { return knobs().gf8_tmap; }
+int gf8_wg_env() { return knobs().gf8_wg; }
+bool gf8_tile_map_set() { return knobs().gf8_tmap_set; }
 }  // namespace detail
 
 int launch(const GfApply& p, hipStream_t s) {
@@ -242,19 +247,27 @@ int launch(const GfApply& p, hipStream_t s) {
         ChunkFn fn;
         if (p.w == 8) {
           fn = gf8_pick(std::make_index_sequence<kMaxK>{}, nk, nr, j0 > 0);
+#ifdef LEOEC_MEASURE
           if (nk == 10 && nr == 4 && j0 == 0) {
-            const int var = gf8_variant_env();
+            const int var = knobs().gf8_variant;
             if (var > 0 && gf8_variant(var)) fn = gf8_variant(var);
           }
+#endif
         } else {
-          const int form = env_int("LEOEC_GFW_FORM", 0);
-          const int cpt = env_int("LEOEC_GFP_CPT", 2);
+          const Knobs& kn = knobs();
+          const int form = kMeasureBuild ? kn.gfw_form : 0;
           if (form == 0)
-            fn = p.w == 16 ? gfp_pick<16>(nr, j0 > 0, cpt) : gfp_pick<32>(nr, j0 > 0, cpt);
+            fn = p.w == 16 ? gfp_pick<16>(nr, j0 > 0, kn.gfp_cpt)
+                           : gfp_pick<32>(nr, j0 > 0, kn.gfp_cpt);
+#ifdef LEOEC_MEASURE
           else if (form == 1 && p.w == 16)
             fn = gf16_pick(nr, j0 > 0);
           else
             fn = p.w == 16 ? gfw_pick<16>(nr, j0 > 0) : gfw_pick<32>(nr, j0 > 0);
+#else
+          else
+            return LEOEC_E_UNSUPPORTED;
+#endif
         }
         const int rc = fn(p, c, s);
         if (rc) return rc;
@@ -279,7 +292,7 @@ LibDecFn lib_dec_kernel(int w) {
 }  // namespace
 
 bool lib_dec_supported(int w) {
-  return env_int("LEOEC_LIB_FORM", 1) != 0 && lib_dec_kernel(w) != nullptr;
+  return knobs().lib_form != 0 && lib_dec_kernel(w) != nullptr;
 }
 
 int launch(const LibDecApply& p, hipStream_t s) {
@@ -304,7 +317,7 @@ int launch(const LibDecApply& p, hipStream_t s) {
     a.nout = nout;
     a.ps = ps;
     a.tiles = tiles;
-    a.xmap = obj_map(tiles, "LEOEC_LIB_XMAP") ? 1u : 0u;
+    a.xmap = obj_map(tiles) ? 1u : 0u;
     uint32_t vmin = 0xFFFFFFFFu;
     auto take = [&](const Shard& sh) {
       if (!sh.base) return DevShard{nullptr, 0, 0, 0};
@@ -334,7 +347,7 @@ int launch(const BitApply& p, hipStream_t s) {
   if (p.block_size == 0 || p.nobj == 0) return LEOEC_OK;
   if (p.block_size % ((uint64_t)16 * w) || p.block_size >= (1ull << 32)) return LEOEC_E_BAD_SIZE;
   if (!shards_ok(p.in) || !shards_ok(p.out)) return LEOEC_E_ARG;
-  if (env_int("LEOEC_LIB_FORM", 1) != 0)
+  if (knobs().lib_form != 0)
     if (const LibFn lf = lib_kernel(w))
       if (is_liberation_encode(p)) return launch_lib(p, lf, s);
   const uint32_t ps = (uint32_t)(p.block_size / (uint64_t)w);
@@ -376,11 +389,13 @@ int launch(const BitApply& p, hipStream_t s) {
         }
         const bool acc = j0 > 0;
         const dim3 grid((uint32_t)(no * tiles)), block(kThreads);
-        const int form = bit_form_env();
+        BitFn fn = bit_kernel_even(std::make_index_sequence<16>{}, RP, acc);
+#ifdef LEOEC_MEASURE
+        // bit_form 8: the shipped form at the {8,16,32} sizes (A/B)
+        const int form = knobs().bit_form;
         const int ro = RP <= 8 ? 8 : RP <= 16 ? 16 : 32;
-        // LEOEC_BIT_FORM=8: the shipped form at the {8,16,32} sizes (A/B)
-        const BitFn fn = form == 4 ? bit_kernel_even(std::make_index_sequence<16>{}, RP, acc)
-                                   : bit_kernel(ro, acc, form == 8 ? 4 : form);
+        if (form != 4) fn = bit_kernel(ro, acc, form == 8 ? 4 : form);
+#endif
         hipLaunchKernelGGL(fn, grid, block, 0, s, a);
         if (hipGetLastError() != hipSuccess) return LEOEC_E_HIP;
       }

@@ -1,0 +1,89 @@
+// knobs.cpp — see knobs.hpp.
+#include "knobs.hpp"
+
+#ifdef LEOEC_MEASURE
+#include <atomic>
+#include <cstdlib>
+#include <mutex>
+#include <string_view>
+#endif
+
+namespace leoec {
+
+#ifndef LEOEC_MEASURE
+
+const Knobs& knobs() {
+  static const Knobs k;  // the shipped forms; the environment is never read
+  return k;
+}
+
+#else
+
+namespace {
+
+int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
+const Knobs* read_env() {
+  Knobs* k = new Knobs;
+  k->bitmatrix = env_int("LEOEC_BITMATRIX", k->bitmatrix);
+  if (const char* e = std::getenv("LEOEC_HOST_STAGING")) {
+    const std::string_view v(e);
+    k->host_staging = v == "pageable" ? 1 : v == "gather" ? 2 : v == "pinned" ? 3 : 0;
+  }
+  k->stage_chunk_kib = env_int("LEOEC_STAGE_CHUNK_KIB", k->stage_chunk_kib);
+  k->batch_window_us = env_int("LEOEC_BATCH_WINDOW_US", k->batch_window_us);
+  k->gf8_variant = env_int("LEOEC_GF8_VARIANT", k->gf8_variant);
+  k->gf8_tmap = env_int("LEOEC_GF8_TMAP", k->gf8_tmap);
+  k->gf8_tmap_set = std::getenv("LEOEC_GF8_TMAP") != nullptr;
+  k->gf8_wg = env_int("LEOEC_GF8_WG", k->gf8_wg);
+  k->gfw_form = env_int("LEOEC_GFW_FORM", k->gfw_form);
+  k->gfp_cpt = env_int("LEOEC_GFP_CPT", k->gfp_cpt);
+  k->gfp_bpc = env_int("LEOEC_GFP_BPC", k->gfp_bpc);
+  k->bit_form = env_int("LEOEC_BIT_FORM", k->bit_form);
+  if (k->bit_form < 0 || k->bit_form > 9) k->bit_form = 4;
+  k->lib_form = env_int("LEOEC_LIB_FORM", k->lib_form);
+  k->lib_la = env_int("LEOEC_LIB_LA", k->lib_la);
+  k->lib_xmap = env_int("LEOEC_LIB_XMAP", k->lib_xmap);
+  k->gfbit_xmap = env_int("LEOEC_GFBIT_XMAP", k->gfbit_xmap);
+  k->gfbit_lw = env_int("LEOEC_GFBIT_LW", k->gfbit_lw);
+  k->gfbit_pf = env_int("LEOEC_GFBIT_PF", k->gfbit_pf);
+  k->gfbit_wg = env_int("LEOEC_GFBIT_WG", k->gfbit_wg);
+  k->gfbit_ceil = env_int("LEOEC_GFBIT_CEIL", k->gfbit_ceil);
+  k->gfbit_lds = env_int("LEOEC_GFBIT_LDS", k->gfbit_lds);
+  return k;
+}
+
+std::atomic<const Knobs*> g_knobs{nullptr};
+std::mutex g_mu;
+
+}  // namespace
+
+const Knobs& knobs() {
+  const Knobs* k = g_knobs.load(std::memory_order_acquire);
+  if (k) return *k;
+  std::lock_guard<std::mutex> lock(g_mu);
+  k = g_knobs.load(std::memory_order_relaxed);
+  if (!k) {
+    k = read_env();
+    g_knobs.store(k, std::memory_order_release);
+  }
+  return *k;
+}
+
+}  // namespace leoec
+
+// Measurement build only: re-read the LEOEC_* variables (a test that changes
+// one between calls).  Earlier snapshots stay valid (they are never freed),
+// so a concurrent launch sees either the old or the new set.
+extern "C" __attribute__((visibility("default"))) void leoec_measure_reload(void) {
+  std::lock_guard<std::mutex> lock(leoec::g_mu);
+  leoec::g_knobs.store(leoec::read_env(), std::memory_order_release);
+}
+
+namespace leoec {
+#endif
+
+}  // namespace leoec

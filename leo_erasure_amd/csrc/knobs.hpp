@@ -1,0 +1,49 @@
+// knobs.hpp — kernel-form and staging-form selectors.
+//
+// The product library (libleoec.so) ships one form of every kernel and one
+// host-staging policy: knobs() returns these compiled-in defaults and the
+// library never reads the environment.  The measurement build
+// (libleoec_measure.so, `make measure`, -DLEOEC_MEASURE) also compiles the
+// alternative forms kept for A/B runs and parity checks, and fills the knobs
+// from LEOEC_* environment variables once, at first use (thread-safe);
+// leoec_measure_reload() re-reads them for a test that changes a variable.
+#pragma once
+
+namespace leoec {
+
+struct Knobs {
+  // engine.cpp
+  int bitmatrix = 0;         // LEOEC_BITMATRIX=1: cauchyrs through the generic bitmatrix kernel
+  int host_staging = 0;      // LEOEC_HOST_STAGING: 0 auto, 1 pageable, 2 gather, 3 pinned ring
+  int stage_chunk_kib = 256; // LEOEC_STAGE_CHUNK_KIB: pinned-ring chunk
+  int batch_window_us = -1;  // LEOEC_BATCH_WINDOW_US: host-call batching window (-1 = default)
+  // kernels.hip / kernels_impl.hpp
+  int gf8_variant = 0;       // LEOEC_GF8_VARIANT: gf8_apply<10,4> variant (gf8_exp.hip)
+  int gf8_tmap = 0;          // LEOEC_GF8_TMAP: gf8_apply workgroup -> tile order
+  bool gf8_tmap_set = false; //   (given: no automatic xcd_obj_map)
+  int gf8_wg = 0;            // LEOEC_GF8_WG=64|256: force the gf8 tile width
+  int gfw_form = 0;          // LEOEC_GFW_FORM: w=16/32 kernel (0 byte-plane gfp_apply)
+  int gfp_cpt = 2;           // LEOEC_GFP_CPT: gfp_apply 16-byte columns per lane
+  int gfp_bpc = 64;          // LEOEC_GFP_BPC: gfp_apply resident blocks per CU
+  int bit_form = 4;          // LEOEC_BIT_FORM: bitmatrix kernel form
+  int lib_form = 1;          // LEOEC_LIB_FORM=0: liberation through the generic bitmatrix kernel
+  int lib_la = 2;            // LEOEC_LIB_LA: lib_apply packet look-ahead
+  int lib_xmap = 2;          // LEOEC_LIB_XMAP=0: liberation kernels without xcd_obj_map
+  // gfbit_inst.hip
+  int gfbit_xmap = -1;       // LEOEC_GFBIT_XMAP: 0 off, 1 object-contiguous, unset auto
+  int gfbit_lw = 2;          // LEOEC_GFBIT_LW: lane width (dwords per packet), w = 8
+  int gfbit_pf = 1;          // LEOEC_GFBIT_PF: blocks of load look-ahead, w = 8
+  int gfbit_wg = 0;          // LEOEC_GFBIT_WG=64: 64-lane workgroups
+  int gfbit_ceil = 0;        // LEOEC_GFBIT_CEIL: traffic-ceiling kernel (not a code)
+  int gfbit_lds = 0;         // LEOEC_GFBIT_LDS=1: LDS-staged inputs
+};
+
+const Knobs& knobs();
+
+#ifdef LEOEC_MEASURE
+constexpr bool kMeasureBuild = true;
+#else
+constexpr bool kMeasureBuild = false;
+#endif
+
+}  // namespace leoec

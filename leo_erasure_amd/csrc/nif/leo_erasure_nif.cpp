@@ -10,6 +10,12 @@
 // {K,M,W} arity is checked, and the NIFs run on dirty schedulers so a GPU
 // round trip never blocks a normal scheduler thread.
 //
+// -DLEOEC_NIF_REF_ERRORS reproduces the reference's error terms exactly: its
+// coder exceptions are rethrown by value as std::exception
+// (nif.cpp:80-83,94-97,108-111), so every coder / engine failure reads
+// "std::exception", and a failed gf_init reads "Galois Initialization
+// Failed! w=8" (nif.cpp:124).  The default keeps the engine's message.
+//
 // Built only where erl_nif.h exists:
 //   c++ -O2 -fPIC -shared -DHAVE_ERL_NIF -I$ERL_ROOT/usr/include -I<repo>/include
 //       leo_erasure_nif.cpp -L<repo>/leo_erasure_amd -lleoec -o priv/leo_erasure.so
@@ -28,6 +34,16 @@ namespace {
 ERL_NIF_TERM error_tuple(ErlNifEnv* env, const char* why) {
   return enif_make_tuple2(env, enif_make_atom(env, "error"),
                           enif_make_string(env, why, ERL_NIF_LATIN1));
+}
+
+// A failure inside the coder (parameter check, block validation, engine).
+ERL_NIF_TERM coder_error(ErlNifEnv* env, int rc) {
+#ifdef LEOEC_NIF_REF_ERRORS
+  (void)rc;
+  return error_tuple(env, "std::exception");
+#else
+  return error_tuple(env, leoec_strerror(rc));
+#endif
 }
 
 // atom -> CodingType numbering (nif.cpp:61-72); -1 = not a known class
@@ -77,7 +93,10 @@ const char* block_lists(ErlNifEnv* env, ERL_NIF_TERM blocks, ERL_NIF_TERM ids,
 
 ERL_NIF_TERM nif_gf_init(ErlNifEnv* env, int, const ERL_NIF_TERM[]) {
   const int rc = leoec_gf_init();
-  return rc ? error_tuple(env, leoec_strerror(rc)) : enif_make_atom(env, "ok");
+#ifdef LEOEC_NIF_REF_ERRORS
+  if (rc) return error_tuple(env, "Galois Initialization Failed! w=8");
+#endif
+  return rc ? coder_error(env, rc) : enif_make_atom(env, "ok");
 }
 
 // encode(Class, {K,M,W}, Bin, TotalSize) -> {ok, [Block]} | {error, Reason}
@@ -85,9 +104,15 @@ ERL_NIF_TERM nif_encode(ErlNifEnv* env, int, const ERL_NIF_TERM argv[]) {
   ErlNifBinary in;
   ERL_NIF_TERM src = argv[2];
   if (!enif_inspect_binary(env, src, &in)) {  // an iolist: flatten it once
-    if (!enif_inspect_iolist_as_binary(env, src, &in)) return error_tuple(env, "Expected Input Bin");
-    src = enif_make_binary(env, &in);  // owned copy, so whole blocks can alias it
-    enif_inspect_binary(env, src, &in);
+    ErlNifBinary flat, owned;
+    if (!enif_inspect_iolist_as_binary(env, src, &flat)) return error_tuple(env, "Expected Input Bin");
+    // The flattened bytes are not a binary the NIF owns (enif_make_binary on
+    // them would yield no term): copy them into one, so whole data blocks can
+    // be sub-binaries of it as for a binary input.
+    if (!enif_alloc_binary(flat.size, &owned)) return coder_error(env, LEOEC_E_NOMEM);
+    if (flat.size) std::memcpy(owned.data, flat.data, flat.size);
+    src = enif_make_binary(env, &owned);
+    if (!enif_inspect_binary(env, src, &in)) return coder_error(env, LEOEC_E_NOMEM);
   }
   int coding, k, m, w;
   if (const char* e = coding_args(env, argv[0], argv[1], &coding, &k, &m, &w))
@@ -95,14 +120,14 @@ ERL_NIF_TERM nif_encode(ErlNifEnv* env, int, const ERL_NIF_TERM argv[]) {
   uint64_t bs;
   int filled;
   int rc = leoec_layout(coding, k, m, w, in.size, &bs, &filled);
-  if (rc) return error_tuple(env, leoec_strerror(rc));
+  if (rc) return coder_error(env, rc);
   ErlNifBinary fresh;
   const size_t fresh_size = (size_t)(k + m - filled) * bs;
-  if (!enif_alloc_binary(fresh_size, &fresh)) return error_tuple(env, leoec_strerror(LEOEC_E_NOMEM));
+  if (!enif_alloc_binary(fresh_size, &fresh)) return coder_error(env, LEOEC_E_NOMEM);
   rc = leoec_encode(coding, k, m, w, in.data, in.size, fresh.data, fresh_size);
   if (rc) {
     enif_release_binary(&fresh);
-    return error_tuple(env, leoec_strerror(rc));
+    return coder_error(env, rc);
   }
   std::vector<ERL_NIF_TERM> out;
   out.reserve(k + m);
@@ -128,16 +153,16 @@ ERL_NIF_TERM nif_decode(ErlNifEnv* env, int, const ERL_NIF_TERM argv[]) {
   const uint64_t bs = bins.empty() ? 0 : bins.back().size;  // rscoding.cpp:102
   std::vector<const uint8_t*> ptrs(bins.size());
   for (size_t i = 0; i < bins.size(); ++i) {
-    if (bins[i].size != bs) return error_tuple(env, leoec_strerror(LEOEC_E_BAD_SIZE));
+    if (bins[i].size != bs) return coder_error(env, LEOEC_E_BAD_SIZE);
     ptrs[i] = bins[i].data;
   }
   ErlNifBinary out;
-  if (!enif_alloc_binary(size, &out)) return error_tuple(env, leoec_strerror(LEOEC_E_NOMEM));
+  if (!enif_alloc_binary(size, &out)) return coder_error(env, LEOEC_E_NOMEM);
   const int rc = leoec_decode(coding, k, m, w, ptrs.data(), ids.data(), (int)ids.size(), bs, size,
                               out.data);
   if (rc) {
     enif_release_binary(&out);
-    return error_tuple(env, leoec_strerror(rc));
+    return coder_error(env, rc);
   }
   return enif_make_tuple2(env, enif_make_atom(env, "ok"), enif_make_binary(env, &out));
 }
@@ -161,16 +186,16 @@ ERL_NIF_TERM nif_repair(ErlNifEnv* env, int, const ERL_NIF_TERM argv[]) {
   const uint64_t bs = bins.empty() ? 0 : bins.back().size;
   std::vector<const uint8_t*> ptrs(bins.size());
   for (size_t i = 0; i < bins.size(); ++i) {
-    if (bins[i].size != bs) return error_tuple(env, leoec_strerror(LEOEC_E_BAD_SIZE));
+    if (bins[i].size != bs) return coder_error(env, LEOEC_E_BAD_SIZE);
     ptrs[i] = bins[i].data;
   }
   ErlNifBinary out;
-  if (!enif_alloc_binary((size_t)nrep * bs, &out)) return error_tuple(env, leoec_strerror(LEOEC_E_NOMEM));
+  if (!enif_alloc_binary((size_t)nrep * bs, &out)) return coder_error(env, LEOEC_E_NOMEM);
   const int rc = leoec_repair(coding, k, m, w, ptrs.data(), ids.data(), (int)ids.size(), bs,
                               rep.data(), (int)nrep, out.data);
   if (rc) {
     enif_release_binary(&out);
-    return error_tuple(env, leoec_strerror(rc));
+    return coder_error(env, rc);
   }
   const ERL_NIF_TERM all = enif_make_binary(env, &out);
   std::vector<ERL_NIF_TERM> blocks(nrep);

@@ -34,15 +34,31 @@ def _cid(coding):
 
 
 def _row_stride(t):
-    assert t.dtype == torch.uint8 and t.is_cuda, "uint8 device tensor expected"
-    assert t.dim() == 2 and t.stride(1) == 1, "2-D row-contiguous tensor expected"
+    if t.dtype != torch.uint8 or not t.is_cuda:
+        raise ValueError("uint8 device tensor expected")
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError("2-D row-contiguous tensor expected")
+    if t.device.index != torch.cuda.current_device():
+        raise ValueError(f"tensor on {t.device}, current device is cuda:{torch.cuda.current_device()}")
     return t.stride(0)
+
+
+def _rows(t, nobj, cols, what):
+    """The kernels read / write `cols` bytes of each of `nobj` rows: the
+    tensor must hold them (the C ABI sees only pointers and strides)."""
+    if nobj < 0 or nobj > t.shape[0]:
+        raise ValueError(f"{what}: nobj {nobj} outside [0, {t.shape[0]}]")
+    if nobj and t.shape[1] < cols:
+        raise ValueError(f"{what}: rows of {t.shape[1]} B, {cols} B needed")
 
 
 def encode(coding, params, objs, size, parity, nobj=None, stream=None):
     """leoec_encode_dev: coding blocks of every object of the batch."""
     k, m, w = params
     nobj = objs.shape[0] if nobj is None else nobj
+    bs, _ = layout(coding, params, size)
+    _rows(objs, nobj, size, "objs")
+    _rows(parity, nobj, m * bs, "parity")
     _lib.check(lib.leoec_encode_dev(_cid(coding), k, m, w, objs.data_ptr(), _row_stride(objs),
                                     size, nobj, parity.data_ptr(), _row_stride(parity),
                                     _stream(stream)))
@@ -52,6 +68,9 @@ def decode(coding, params, objs, size, parity, erased, nobj=None, stream=None):
     """leoec_decode_dev: rebuild the erased data blocks in place in ``objs``."""
     k, m, w = params
     nobj = objs.shape[0] if nobj is None else nobj
+    bs, _ = layout(coding, params, size)
+    _rows(objs, nobj, size, "objs")
+    _rows(parity, nobj, m * bs, "parity")
     er = (ctypes.c_int * max(len(erased), 1))(*erased)
     _lib.check(lib.leoec_decode_dev(_cid(coding), k, m, w, objs.data_ptr(), _row_stride(objs),
                                     size, nobj, parity.data_ptr(), _row_stride(parity), er,
@@ -65,7 +84,15 @@ def repair(coding, params, blocks, block_size, repair_ids, out, nobj, stream=Non
     k, m, w = params
     strides = {_row_stride(b) for b in blocks if b is not None}
     ostrides = {_row_stride(o) for o in out}
-    assert len(strides) == 1 and len(ostrides) == 1, "one row stride per side expected"
+    if len(strides) != 1 or len(ostrides) != 1:
+        raise ValueError("one row stride per side expected")
+    if len(blocks) != k + m:
+        raise ValueError(f"blocks: {k + m} entries (tensor or None) expected")
+    for b in blocks:
+        if b is not None:
+            _rows(b, nobj, block_size, "block")
+    for o in out:
+        _rows(o, nobj, block_size, "out")
     ptrs = (ctypes.c_void_p * (k + m))(*[b.data_ptr() if b is not None else None for b in blocks])
     optrs = (ctypes.c_void_p * max(len(out), 1))(*[o.data_ptr() for o in out])
     rep = (ctypes.c_int * max(len(repair_ids), 1))(*repair_ids)

@@ -129,10 +129,12 @@ ERL_NIF_TERM enif_make_binary(ErlNifEnv*, ErlNifBinary* bin) {
       return put(std::move(t));
     }
   }
-  // An inspected (not owned) binary: the VM would copy or share it; copy.
-  t.owner = new_owner(bin->size);
-  if (bin->size) std::memcpy(t.owner->bytes.data(), bin->data, bin->size);
-  return put(std::move(t));
+  // Not an enif_alloc_binary'd buffer (e.g. the result of
+  // enif_inspect_iolist_as_binary): real ERTS returns THE_NON_VALUE here,
+  // which crashes the VM once used as a term.  Count it and hand back the
+  // invalid handle 0.
+  ++g_violations;
+  return 0;
 }
 
 ERL_NIF_TERM enif_make_sub_binary(ErlNifEnv*, ERL_NIF_TERM bin, size_t pos, size_t size) {

@@ -27,11 +27,13 @@ class Atom(str):
         return f"Atom({str(self)!r})"
 
 
-def build(outdir):
-    so = os.path.join(outdir, "libnif_harness.so")
+def build(outdir, defines=()):
+    """defines: extra -D flags for the shim, e.g. ("LEOEC_NIF_REF_ERRORS",)."""
+    so = os.path.join(outdir, "libnif_harness%s.so" % "".join("_" + d.lower() for d in defines))
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fPIC", "-shared", "-Wall", "-Werror",
-           "-DHAVE_ERL_NIF", "-I", HERE, "-I", os.path.join(ROOT, "include"),
-           os.path.join(HERE, "harness.cpp"), SHIM, "-o", so]
+           "-DHAVE_ERL_NIF", "-I", HERE, "-I", os.path.join(ROOT, "include")]
+    cmd += ["-D" + d for d in defines]
+    cmd += [os.path.join(HERE, "harness.cpp"), SHIM, "-o", so]
     subprocess.run(cmd, check=True, capture_output=True, text=True)
     return so
 

@@ -266,11 +266,11 @@ def test_device_roundtrip_bench_shape(gpu, le):
                                  {"LEOEC_BITMATRIX": "1", "LEOEC_BIT_FORM": "1"},
                                  {"LEOEC_BITMATRIX": "1", "LEOEC_BIT_FORM": "2"}],
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
-def test_cauchy_kernel_forms_agree(gpu, le, oracle, env, monkeypatch):
+def test_cauchy_kernel_forms_agree(gpu, le, oracle, env, measure):
     """cauchyrs through the generic masked-bitmatrix kernel and through every
     lane width of the bitsliced GF kernel gives the oracle's bytes."""
     for k, v in env.items():
-        monkeypatch.setenv(k, v)
+        measure.setenv(k, v)
     for cls, k, m, w in [("cauchyrs", 10, 4, 8), ("cauchyrs", 6, 3, 4), ("cauchyrs", 4, 2, 3)]:
         data = rand_bytes(100003, k + m + w)
         st, blocks = le.nif_encode(cls, (k, m, w), data, len(data))
@@ -281,10 +281,10 @@ def test_cauchy_kernel_forms_agree(gpu, le, oracle, env, monkeypatch):
 
 
 @pytest.mark.parametrize("form", ["0", "1", "2", "3", "4", "5", "6", "7", "8"])
-def test_bitmatrix_kernel_forms_agree(gpu, le, oracle, form, monkeypatch):
+def test_bitmatrix_kernel_forms_agree(gpu, le, oracle, form, measure):
     """liberation (and >32 output packets: w = 17 cauchy) through every form of
     the bitmatrix kernel: masked / branchy, with and without look-ahead."""
-    monkeypatch.setenv("LEOEC_BIT_FORM", form)
+    measure.setenv("LEOEC_BIT_FORM", form)
     for cls, k, m, w in [("liberation", 7, 2, 7), ("liberation", 3, 2, 31),
                          ("cauchyrs", 5, 3, 17)]:
         data = rand_bytes(150001, k + w)
@@ -298,12 +298,12 @@ def test_bitmatrix_kernel_forms_agree(gpu, le, oracle, form, monkeypatch):
 
 
 @pytest.mark.parametrize("form", ["0", "1"])
-def test_liberation_encode_forms(gpu, le, oracle, form, monkeypatch):
+def test_liberation_encode_forms(gpu, le, oracle, form, measure):
     """lib_apply (the liberation bitmatrix structure compiled in, LEOEC_LIB_FORM=1,
     shipped) and the generic masked bitmatrix kernel (0): every instantiated w,
     k from 1 to w, sizes with ragged tails, against the oracle; decode and
     repair (generic kernel) of what was encoded."""
-    monkeypatch.setenv("LEOEC_LIB_FORM", form)
+    measure.setenv("LEOEC_LIB_FORM", form)
     for w in (3, 5, 7, 11, 13):
         for k in sorted({1, 2, (w + 1) // 2, w}):
             for size in (1, 4097, 150001):
@@ -328,7 +328,7 @@ def test_liberation_encode_forms(gpu, le, oracle, form, monkeypatch):
                 assert st == "ok" and rep == [blocks[1]], (k, w)
 
 
-def test_liberation_device_batch_forms(gpu, le, oracle, monkeypatch):
+def test_liberation_device_batch_forms(gpu, le, oracle, measure):
     """Device-resident batch (ragged object size, 37 objects) through both
     liberation encode forms: identical parity, equal to the oracle."""
     k, m, w = 7, 2, 7
@@ -337,7 +337,7 @@ def test_liberation_device_batch_forms(gpu, le, oracle, monkeypatch):
     host, objs = _batch(gpu, n, size, size + 9 - (size + 9) % 16 + 16, 21)
     outs = []
     for form in ("1", "0"):
-        monkeypatch.setenv("LEOEC_LIB_FORM", form)
+        measure.setenv("LEOEC_LIB_FORM", form)
         parity = gpu.full((n, m * bs), 0x5A, dtype=gpu.uint8, device="cuda")
         le.device.encode("liberation", (k, m, w), objs, size, parity)
         gpu.cuda.synchronize()
@@ -349,12 +349,12 @@ def test_liberation_device_batch_forms(gpu, le, oracle, monkeypatch):
 
 
 @pytest.mark.parametrize("wg", ["64", "256"])
-def test_gf8_tile_width_forms(gpu, le, oracle, wg, monkeypatch):
+def test_gf8_tile_width_forms(gpu, le, oracle, wg, measure):
     """gf8_apply at both tile widths (64-lane workgroups are shipped for blocks
     above 160 KiB, 256-lane below; LEOEC_GF8_WG forces one): sizes either side
     of the switch, encode against the oracle, a 4-data-erasure decode round
     trip and a data+parity repair."""
-    monkeypatch.setenv("LEOEC_GF8_WG", wg)
+    measure.setenv("LEOEC_GF8_WG", wg)
     for cls, k, m in [("vandrs", 10, 4), ("isars", 10, 4), ("vandrs", 4, 2), ("vandrs", 17, 5)]:
         for size in (1, 5000, 1048576, 2097152 + 12345):
             data = rand_bytes(size, size + k)
@@ -369,7 +369,7 @@ def test_gf8_tile_width_forms(gpu, le, oracle, wg, monkeypatch):
 
 @pytest.mark.parametrize("cls,k,m,w", [("vandrs", 10, 4, 8), ("cauchyrs", 10, 4, 8),
                                        ("liberation", 7, 2, 7)])
-def test_xcd_object_map_batches(gpu, le, oracle, monkeypatch, cls, k, m, w):
+def test_xcd_object_map_batches(gpu, le, oracle, measure, cls, k, m, w):
     """The object-interleaved XCD map (objects of <= 64 tiles) on batches that
     are not a multiple of 8 objects (the tail keeps dispatch order): parity
     identical with the map off, equal to the oracle, and decode in place."""
@@ -381,9 +381,9 @@ def test_xcd_object_map_batches(gpu, le, oracle, monkeypatch, cls, k, m, w):
     for env in (None, "0"):
         for var in ("LEOEC_GF8_TMAP", "LEOEC_GFBIT_XMAP", "LEOEC_LIB_XMAP"):
             if env is None:
-                monkeypatch.delenv(var, raising=False)
+                measure.delenv(var, raising=False)
             else:
-                monkeypatch.setenv(var, env)
+                measure.setenv(var, env)
         parity = gpu.zeros((n, max(k, m) * bs), dtype=gpu.uint8, device="cuda")
         le.device.encode(cls, (k, m, w), objs, size, parity)
         objs[:, :2 * bs] = 0
@@ -432,12 +432,12 @@ def test_file_helpers(gpu, le, tmp_path, monkeypatch):
     {"LEOEC_GFW_FORM": "1"},                   # w=16: 2-bit-field v_perm; w=32: shift-and-add
     {"LEOEC_GFW_FORM": "2"},                   # shift-and-add
 ])
-def test_gfw_kernel_forms_agree(gpu, le, oracle, w, env, monkeypatch):
+def test_gfw_kernel_forms_agree(gpu, le, oracle, w, env, measure):
     """w = 16 / 32 through every kernel form: encode vs the oracle, decode
     and repair round trips, including > 16 inputs (accumulating launches,
     whose outputs are re-read into byte planes) and ragged tails."""
     for key, val in env.items():
-        monkeypatch.setenv(key, val)
+        measure.setenv(key, val)
     for k, m, size in [(10, 4, 200011), (4, 2, 77777), (17, 5, 123457), (3, 3, 1000)]:
         data = rand_bytes(size, k * m + w)
         st, blocks = le.nif_encode("vandrs", (k, m, w), data, len(data))
@@ -528,7 +528,7 @@ def test_concurrent_callers(gpu, le, oracle):
 @pytest.mark.parametrize("staging,chunk_kib", [("pinned", "16"), ("pinned", "256"),
                                                ("pinned", "8192"), ("pageable", "256"),
                                                ("gather", "256"), ("auto", "256")])
-def test_host_staging_forms(gpu, le, oracle, staging, chunk_kib, monkeypatch):
+def test_host_staging_forms(gpu, le, oracle, staging, chunk_kib, measure):
     """Host entry points (the NIF path) under every staging form: the plain
     pageable copies, the default (auto: gather for several host buffers),
     the gather form (one pinned copy per direction,
@@ -536,8 +536,8 @@ def test_host_staging_forms(gpu, le, oracle, staging, chunk_kib, monkeypatch):
     measurement form with chunks small enough to wrap the 8-slot ring many
     times within one call, and one chunk per object.  Encode / decode / repair bit-exact with the
     oracle, including ragged sizes and a 64 MiB + 5 object."""
-    monkeypatch.setenv("LEOEC_HOST_STAGING", staging)
-    monkeypatch.setenv("LEOEC_STAGE_CHUNK_KIB", chunk_kib)
+    measure.setenv("LEOEC_HOST_STAGING", staging)
+    measure.setenv("LEOEC_STAGE_CHUNK_KIB", chunk_kib)
     cases = [("vandrs", 10, 4, 8, 1048576), ("vandrs", 10, 4, 8, 300001),
              ("cauchyrs", 10, 4, 8, 1048576 + 77), ("isars", 4, 2, 8, 65536 + 7),
              ("liberation", 4, 2, 7, 777777), ("vandrs", 6, 3, 32, 123457)]

@@ -28,17 +28,26 @@ def nif(tmp_path_factory, le):
     h.L.h_reset()
 
 
+@pytest.fixture(scope="module")
+def nif_ref(tmp_path_factory, le):
+    """The shim built with -DLEOEC_NIF_REF_ERRORS (the reference's error terms)."""
+    so = build(str(tmp_path_factory.mktemp("nif_ref")), ("LEOEC_NIF_REF_ERRORS",))
+    h = Harness(so)
+    yield h
+    h.L.h_reset()
+
+
 @pytest.fixture(autouse=True)
 def _fresh(request):
-    if "nif" in request.fixturenames:
-        h = request.getfixturevalue("nif")
+    hs = [request.getfixturevalue(n) for n in ("nif", "nif_ref") if n in request.fixturenames]
+    for h in hs:
         h.L.h_reset()
-        yield
-        # every enif_alloc_binary was either handed to the VM or released
+    yield
+    for h in hs:
+        # every enif_alloc_binary was either handed to the VM or released, and
+        # no term was made from a buffer the NIF does not own
         assert h.L.h_live_allocs() == 0
         assert h.L.h_violations() == 0
-    else:
-        yield
 
 
 def err(r):
@@ -160,6 +169,49 @@ def test_python_mirror_agrees(le, fn, table):
     # The mirror takes str for atoms; every case above keeps its meaning.
     for args, reason in table:
         assert getattr(le, fn)(*_py(args)) == ("error", reason), (fn, args)
+
+
+@pytest.mark.parametrize("args,reason", ENCODE_ERRORS, ids=[r for _, r in ENCODE_ERRORS])
+def test_ref_errors_build_keeps_argument_errors(nif_ref, args, reason):
+    """-DLEOEC_NIF_REF_ERRORS changes only coder errors: argument errors and
+    "Invalid Coding" (thrown outside the coder, nif.cpp:71,158-161) keep
+    their text."""
+    assert err(nif_ref.call("encode", *args)) == reason
+
+
+@pytest.mark.parametrize("cls,params", [("vandrs", (10, 4, 7)), ("liberation", (4, 2, 8)),
+                                        ("isars", (10, 4, 16))])
+def test_ref_errors_build_slices_coder_errors(nif_ref, nif, cls, params):
+    """Coder exceptions rethrown by value read "std::exception" in the
+    reference (nif.cpp:80-83); the default build keeps the coder's text."""
+    assert err(nif_ref.call("encode", Atom(cls), params, DATA, len(DATA))) == "std::exception"
+    assert err(nif.call("encode", Atom(cls), params, DATA, len(DATA))) != "std::exception"
+    r = nif_ref.call("decode", Atom(cls), params, [b"abcd", b"abc"], [0, 1], 7)
+    assert err(r) == "std::exception"
+    r = nif_ref.call("repair", Atom(cls), params, [b"abcd", b"abc"], [0, 1], [2])
+    assert err(r) == "std::exception"
+
+
+def test_ref_errors_build_gf_init(nif_ref, le):
+    r = nif_ref.call("gf_init")
+    if le.gf_init() == "ok":
+        assert r == ok
+    else:  # nif.cpp:124
+        assert err(r) == "Galois Initialization Failed! w=8"
+
+
+def test_iolist_input_is_copied_into_an_owned_binary(nif, le):
+    """An iolist encode input is flattened into a binary the NIF allocates
+    (enif_make_binary on the flattened view is no term in ERTS); the harness
+    counts a violation otherwise.  Without a GPU the call then fails in the
+    engine, after the copy."""
+    r = nif.call("encode", VANDRS, PARAMS, [b"ab", [99, b"def"], b""], 6)
+    if le.gf_init() == "ok":
+        assert r[0] == ok and b"".join(bytes(b) for b in r[1][:1])[:6] == b"abcdef"
+    else:
+        assert err(r) == le.strerror(-16)
+    r = nif.call("encode", VANDRS, PARAMS, [], 0)  # empty iolist
+    assert r[0] == ok and len(r[1]) == 14 and all(len(b) == 0 for b in r[1])
 
 
 def test_mismatched_block_sizes(nif, le):
