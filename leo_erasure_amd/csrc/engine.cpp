@@ -16,6 +16,7 @@
 #include <tuple>
 
 #include "../../include/leoec.h"
+#include "hostq.hpp"
 #include "knobs.hpp"
 
 namespace leoec {
@@ -666,15 +667,38 @@ int run_host_map(const Code& c, const uint8_t* const* blocks, const std::vector<
     in[i] = Shard{st->buf + (uint64_t)i * bs16, 0, bs};
   }
   rc = stage_h2d_segs(st, st->buf, segs);
-  if (rc) return rc;
   uint8_t* outbase = st->buf + (uint64_t)k * bs16;
   for (size_t o = 0; o < want.size(); ++o) out[o] = Shard{outbase + o * bs16, 0, bs};
-  rc = apply(c, surv.data(), in, want.data(), out, bs16, 1, st->stream);
-  if (rc) return rc;
+  if (rc == LEOEC_OK) rc = apply(c, surv.data(), in, want.data(), out, bs16, 1, st->stream);
+  if (rc) {
+    // copies already queued may still read this thread's pinned buffer:
+    // drain them before the next call reuses it
+    (void)hipStreamSynchronize(st->stream);
+    return rc;
+  }
   *st_out = st;
   *dev_out = outbase;
   *stride_out = bs16;
   return LEOEC_OK;
+}
+
+// The batched form of run_host_map's map (outputs left to the caller): the k
+// survivor blocks packed at bs16 spacing, outputs at bs16 spacing.
+void host_map_job(const Code& c, const uint8_t* const* blocks, const std::vector<int>& surv,
+                  const std::vector<int>& slot, const std::vector<int>& want, uint64_t bs,
+                  HostJob* J) {
+  const uint64_t bs16 = round_to(bs, 16);
+  const int k = c.k;
+  J->code = &c;
+  J->surv = surv;
+  J->want = want;
+  J->bs = J->in_blk = J->out_blk = bs16;
+  J->in_valid.assign(k, bs);
+  J->out_valid = bs;
+  J->in_bytes = (uint64_t)k * bs16;
+  J->out_bytes = (uint64_t)want.size() * bs16;
+  J->direct_cap = knobs().hostq_direct_map;
+  for (int i = 0; i < k; ++i) J->in.push_back(HostSeg{blocks[slot[i]], (uint64_t)i * bs16, bs});
 }
 
 }  // namespace
@@ -717,23 +741,38 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
   std::memset(out, 0, tail_bytes);
   std::memcpy(out, obj + (uint64_t)filled * bs, size - (uint64_t)filled * bs);
 
+  std::vector<int> surv(k), want(m);
+  for (int j = 0; j < k; ++j) surv[j] = j;
+  for (int i = 0; i < m; ++i) want[i] = k + i;
+  HostqTicket ticket;
+  {  // concurrent calls: one batched H2D / launch / D2H (hostq.cpp)
+    HostJob J;
+    J.code = c;
+    J.surv = surv;
+    J.want = want;
+    J.bs = J.in_blk = J.out_blk = J.out_valid = bs;
+    for (int j = 0; j < k; ++j) J.in_valid.push_back(clamp_valid(size, (uint64_t)j * bs, bs));
+    J.in_bytes = round_to(size, 16);
+    J.out_bytes = (uint64_t)m * bs;
+    J.in.push_back(HostSeg{obj, 0, size});
+    J.out.push_back(OutSeg{out + tail_bytes, 0, (uint64_t)m * bs});
+    J.direct_cap = knobs().hostq_direct;
+    rc = hostq_run(J, &ticket);
+    if (rc != kNotBatched) return rc;
+  }
   Staging* st;
   rc = get_staging((size_t)(k + m) * bs, &st);
   if (rc) return rc;
-  rc = stage_h2d_segs(st, st->buf, {H2DSeg{obj, 0, (size_t)size}});
-  if (rc) return rc;
   std::vector<Shard> in(k), par(m);
-  std::vector<int> surv(k), want(m);
-  for (int j = 0; j < k; ++j) {
+  for (int j = 0; j < k; ++j)
     in[j] = Shard{st->buf + (uint64_t)j * bs, 0, clamp_valid(size, (uint64_t)j * bs, bs)};
-    surv[j] = j;
+  for (int i = 0; i < m; ++i) par[i] = Shard{st->buf + (uint64_t)(k + i) * bs, 0, bs};
+  rc = stage_h2d_segs(st, st->buf, {H2DSeg{obj, 0, (size_t)size}});
+  if (rc == LEOEC_OK) rc = apply(*c, surv.data(), in, want.data(), par, bs, 1, st->stream);
+  if (rc) {
+    (void)hipStreamSynchronize(st->stream);  // queued copies may still read the caller's object
+    return rc;
   }
-  for (int i = 0; i < m; ++i) {
-    par[i] = Shard{st->buf + (uint64_t)(k + i) * bs, 0, bs};
-    want[i] = k + i;
-  }
-  rc = apply(*c, surv.data(), in, want.data(), par, bs, 1, st->stream);
-  if (rc) return rc;
   return stage_d2h_sync(st, {D2HSeg{out + tail_bytes, st->buf + (uint64_t)k * bs,
                                     (size_t)((uint64_t)m * bs)}});
 }
@@ -754,24 +793,46 @@ int op_decode(int coding, int k, int m, int w, const uint8_t* const* blocks, con
   std::vector<int> want;
   for (int i = 0; i < k; ++i)
     if (present[i] < 0 && (uint64_t)i * bs < size) want.push_back(i);
+  // surviving data blocks: host copies (overlapping the GPU work when there is some)
+  struct Survivors {
+    int k;
+    uint64_t bs, size;
+    const uint8_t* const* blocks;
+    const std::vector<int>* present;
+    uint8_t* out;
+    static void copy(void* p) {
+      const Survivors& v = *static_cast<const Survivors*>(p);
+      for (int i = 0; i < v.k; ++i) {
+        const uint64_t off = (uint64_t)i * v.bs;
+        if (off >= v.size) break;
+        if ((*v.present)[i] >= 0)
+          std::memcpy(v.out + off, v.blocks[(*v.present)[i]], clamp_valid(v.size, off, v.bs));
+      }
+    }
+  } survivors{k, bs, size, blocks, &present, out};
   Staging* st = nullptr;
   uint8_t* dev = nullptr;
   uint64_t dstride = 0;
+  HostqTicket ticket;
   if (!want.empty()) {
     const Code* c;
     rc = get_code(coding, k, m, w, &c);
     if (rc) return rc;
     std::vector<int> surv, slot;
     pick_survivors(coding, k, ids, present, &surv, &slot);
+    const uint64_t bs16 = round_to(bs, 16);
+    if (c->bitmatrix && (bs % (16ull * (uint64_t)w))) return LEOEC_E_BAD_SIZE;
+    HostJob J;
+    host_map_job(*c, blocks, surv, slot, want, bs, &J);
+    for (size_t o = 0; o < want.size(); ++o)
+      J.out.push_back(OutSeg{out + (uint64_t)want[o] * bs, o * bs16,
+                             clamp_valid(size, (uint64_t)want[o] * bs, bs)});
+    rc = hostq_run(J, &ticket, &Survivors::copy, &survivors);
+    if (rc != kNotBatched) return rc;
     rc = run_host_map(*c, blocks, surv, slot, want, bs, &st, &dev, &dstride);
     if (rc) return rc;
   }
-  // surviving data blocks: host copies, overlapping the kernel
-  for (int i = 0; i < k; ++i) {
-    const uint64_t off = (uint64_t)i * bs;
-    if (off >= size) break;
-    if (present[i] >= 0) std::memcpy(out + off, blocks[present[i]], clamp_valid(size, off, bs));
-  }
+  Survivors::copy(&survivors);
   if (!st) return LEOEC_OK;
   std::vector<D2HSeg> segs;
   for (size_t o = 0; o < want.size(); ++o) {
@@ -811,6 +872,17 @@ int op_repair(int coding, int k, int m, int w, const uint8_t* const* blocks, con
   if (rc) return rc;
   std::vector<int> surv, slot;
   pick_survivors(coding, k, ids, present, &surv, &slot);
+  if (c->bitmatrix && (bs % (16ull * (uint64_t)w))) return LEOEC_E_BAD_SIZE;
+  HostqTicket ticket;
+  {
+    const uint64_t bs16 = round_to(bs, 16);
+    HostJob J;
+    host_map_job(*c, blocks, surv, slot, want, bs, &J);
+    for (size_t o = 0; o < want.size(); ++o)
+      J.out.push_back(OutSeg{out + (uint64_t)pos[o] * bs, o * bs16, bs});
+    rc = hostq_run(J, &ticket);
+    if (rc != kNotBatched) return rc;
+  }
   Staging* st;
   uint8_t* dev;
   uint64_t dstride;

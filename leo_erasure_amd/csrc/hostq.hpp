@@ -1,0 +1,75 @@
+// hostq.hpp — cross-call batching of the host-memory entry points.
+//
+// The reference is called once per object, from many scheduler threads at
+// once (basho_bench {concurrent, 4}: test/basho_bench_leo_erasure_rs_10_4_8_
+// 1M_w_t4.config:24), and every call starts and ends in host memory
+// (c_src/rscoding.cpp:41,73-81).  One PCIe round trip per object costs
+// ~15-20 us of copy submit + wait per copy whatever its size, so concurrent
+// calls are packed: each device has a queue whose worker thread takes every
+// call that arrived while the previous batch was on the GPU, and moves the
+// batch with ONE H2D, one launch per run of identical maps (nobj > 1), and
+// ONE D2H.  Callers pack their own inputs into the batch's pinned buffer and
+// unpack their outputs (host memcpys run in parallel on the callers'
+// threads); the worker only issues copies and launches.  A lone caller pays
+// no window: a batch closes as soon as the GPU has room for it.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "engine.hpp"
+
+namespace leoec {
+
+struct HostSeg {  // caller buffer -> job input region
+  const uint8_t* src;
+  uint64_t off, n;
+};
+struct OutSeg {  // job output region -> caller buffer
+  uint8_t* dst;
+  uint64_t off, n;
+};
+
+// One call's map: out block o = map(surv -> want[o]) applied to k input
+// blocks.  Input block i lives at in_blk * i inside the job's input region
+// (in_valid[i] bytes of it are real, the rest read as zero), output block o
+// at out_blk * o inside its output region.
+struct HostJob {
+  const Code* code = nullptr;
+  std::vector<int> surv, want;
+  uint64_t bs = 0;  // kernel block geometry (multiple of 16)
+  uint64_t in_blk = 0, out_blk = 0;
+  std::vector<uint64_t> in_valid;  // per input block
+  uint64_t out_valid = 0;          // per output block
+  uint64_t in_bytes = 0, out_bytes = 0;
+  std::vector<HostSeg> in;
+  std::vector<OutSeg> out;
+  int direct_cap = 0;  // calls of this kind allowed on the per-thread path at an idle queue
+};
+
+// Largest job input / output region that is batched; larger calls take the
+// per-thread path (their copies amortise their own submit cost).
+constexpr uint64_t kBatchMaxJobBytes = (uint64_t)8 << 20;
+
+// Held by a call that hostq_run sent to its per-thread path while the queue
+// was idle (few concurrent callers: their own streams and direct copies are
+// faster than a batch); released when the call returns.
+struct HostqTicket {
+  void* queue = nullptr;
+  HostqTicket() = default;
+  HostqTicket(const HostqTicket&) = delete;
+  HostqTicket& operator=(const HostqTicket&) = delete;
+  ~HostqTicket();
+};
+
+// Run `job` through the current device's queue and wait for it.  `overlap`
+// (may be null) runs on the caller's thread while the batch is on the GPU.
+// Returns a leoec_status, or kNotBatched: nothing was done and the caller
+// runs its per-thread path — the job is too large, batching is off, pinned
+// memory is short, or the queue is idle and fewer than job.direct_cap
+// calls are already running direct (`ticket` then counts this one).
+constexpr int kNotBatched = 1;
+int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*) = nullptr,
+              void* arg = nullptr);
+
+}  // namespace leoec

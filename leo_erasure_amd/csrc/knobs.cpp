@@ -34,7 +34,14 @@ const Knobs* read_env() {
     k->host_staging = v == "pageable" ? 1 : v == "gather" ? 2 : v == "pinned" ? 3 : 0;
   }
   k->stage_chunk_kib = env_int("LEOEC_STAGE_CHUNK_KIB", k->stage_chunk_kib);
+  k->host_batch = env_int("LEOEC_HOST_BATCH", k->host_batch);
   k->batch_window_us = env_int("LEOEC_BATCH_WINDOW_US", k->batch_window_us);
+  k->hostq_depth = env_int("LEOEC_HOSTQ_DEPTH", k->hostq_depth);
+  if (k->hostq_depth < 1 || k->hostq_depth > 3) k->hostq_depth = 3;
+  k->hostq_sync = env_int("LEOEC_HOSTQ_SYNC", k->hostq_sync);
+  k->hostq_close = env_int("LEOEC_HOSTQ_CLOSE", k->hostq_close);
+  k->hostq_direct = env_int("LEOEC_HOSTQ_DIRECT", k->hostq_direct);
+  k->hostq_direct_map = env_int("LEOEC_HOSTQ_DIRECT_MAP", k->hostq_direct_map);
   k->gf8_variant = env_int("LEOEC_GF8_VARIANT", k->gf8_variant);
   k->gf8_tmap = env_int("LEOEC_GF8_TMAP", k->gf8_tmap);
   k->gf8_tmap_set = std::getenv("LEOEC_GF8_TMAP") != nullptr;

@@ -16,7 +16,17 @@ struct Knobs {
   int bitmatrix = 0;         // LEOEC_BITMATRIX=1: cauchyrs through the generic bitmatrix kernel
   int host_staging = 0;      // LEOEC_HOST_STAGING: 0 auto, 1 pageable, 2 gather, 3 pinned ring
   int stage_chunk_kib = 256; // LEOEC_STAGE_CHUNK_KIB: pinned-ring chunk
-  int batch_window_us = -1;  // LEOEC_BATCH_WINDOW_US: host-call batching window (-1 = default)
+  int host_batch = 1;        // LEOEC_HOST_BATCH=0: host calls take the per-thread path only
+  int batch_window_us = 0;   // LEOEC_BATCH_WINDOW_US: hold an idle-GPU batch open this long
+  int hostq_depth = 3;       // LEOEC_HOSTQ_DEPTH: batches on the GPU at once
+  int hostq_sync = 1;        // LEOEC_HOSTQ_SYNC: 1 poll events (hipEventQuery + yield),
+                             //   0 hipEventSynchronize
+  int hostq_close = 1;       // LEOEC_HOSTQ_CLOSE: 1 close a batch when the previous H2D is
+                             //   done, 0 as soon as the GPU has room
+  int hostq_direct = 4;      // LEOEC_HOSTQ_DIRECT: encode calls that may take the per-thread
+                             //   path while the queue is idle (0: every call batched)
+  int hostq_direct_map = 2;  // LEOEC_HOSTQ_DIRECT_MAP: the same for decode / repair (their
+                             //   per-thread path gathers k buffers: it tops out sooner)
   // kernels.hip / kernels_impl.hpp
   int gf8_variant = 0;       // LEOEC_GF8_VARIANT: gf8_apply<10,4> variant (gf8_exp.hip)
   int gf8_tmap = 0;          // LEOEC_GF8_TMAP: gf8_apply workgroup -> tile order

@@ -634,3 +634,96 @@ def test_bench_encode_100MiB_zero(gpu, le):
         ids = list(range(m, k + m))
         st, out = le.nif_decode(cls, (k, m, w), [blocks[i] for i in ids], ids, size)
         assert st == "ok" and out == data, cls
+
+
+def _capi_case(le, oracle, cls, k, m, w, size, seed):
+    """Inputs and oracle answers for one object, as numpy buffers for the C ABI."""
+    data = np.frombuffer(rand_bytes(size, seed), dtype=np.uint8).copy()
+    ref = oracle.encode(cls, k, m, w, data.tobytes())
+    bs, filled = le.layout(cls, (k, m, w), size)
+    return {"cls": cls, "cid": le._lib.CODING_IDS[cls], "p": (k, m, w), "size": size, "bs": bs,
+            "filled": filled, "data": data, "ref": ref,
+            "blocks": [np.frombuffer(b, dtype=np.uint8).copy() for b in ref]}
+
+
+def _capi_roundtrip(le, c, t):
+    """encode + decode (m blocks lost) + repair (2 blocks) through the C ABI;
+    returns an error string or None."""
+    import ctypes
+    L = le.lib
+    k, m, w = c["p"]
+    bs, filled, size = c["bs"], c["filled"], c["size"]
+    out = np.empty(max((k + m - filled) * bs, 1), dtype=np.uint8)
+    rc = L.leoec_encode(c["cid"], k, m, w, c["data"].ctypes.data, size, out.ctypes.data, out.size)
+    if rc or b"".join(c["ref"][filled:]) != out[:(k + m - filled) * bs].tobytes():
+        return f"encode {c['cls']}{c['p']} size {size} rc {rc}"
+    lost = sorted({(t * 7 + j * 3) % (k + m) for j in range(m)})
+    ids = [b for b in range(k + m) if b not in lost][::-1]
+    ptrs = (ctypes.c_void_p * len(ids))(*[c["blocks"][b].ctypes.data for b in ids])
+    idv = (ctypes.c_int * len(ids))(*ids)
+    dec = np.empty(max(size, 1), dtype=np.uint8)
+    rc = L.leoec_decode(c["cid"], k, m, w, ptrs, idv, len(ids), bs, size, dec.ctypes.data)
+    if rc or not np.array_equal(dec[:size], c["data"]):
+        return f"decode {c['cls']}{c['p']} lost {lost} rc {rc}"
+    rep = sorted({t % (k + m), (t + 5) % (k + m)})
+    avail = [b for b in range(k + m) if b not in rep]
+    ptrs = (ctypes.c_void_p * len(avail))(*[c["blocks"][b].ctypes.data for b in avail])
+    idv = (ctypes.c_int * len(avail))(*avail)
+    repv = (ctypes.c_int * len(rep))(*rep)
+    ro = np.empty(len(rep) * bs, dtype=np.uint8)
+    rc = L.leoec_repair(c["cid"], k, m, w, ptrs, idv, len(avail), bs, repv, len(rep),
+                        ro.ctypes.data)
+    if rc or ro.tobytes() != b"".join(c["ref"][b] for b in rep):
+        return f"repair {c['cls']}{c['p']} {rep} rc {rc}"
+    return None
+
+
+@pytest.mark.parametrize("form", ["product", "always-batch", "per-thread"])
+def test_host_batching_mixed_callers(gpu, le, oracle, form, request):
+    """Cross-call batching (hostq.cpp): 24 threads call the C ABI at once with
+    mixed classes, widths, sizes (ragged, and 9 MiB objects above the batch
+    cap, which take the per-thread path) and erasure patterns, so one batch
+    holds several different maps (several launches) and identical maps are
+    merged into one launch.  Every result equals the oracle's.  The
+    measurement build forces every call through the queue (always-batch) or
+    none (per-thread) and reports how calls were batched."""
+    import concurrent.futures as cf
+    stats = None
+    if form != "product":
+        ms = request.getfixturevalue("measure")
+        if form == "always-batch":
+            ms.setenv("LEOEC_HOSTQ_DIRECT", "0")
+            ms.setenv("LEOEC_HOSTQ_DIRECT_MAP", "0")
+        else:
+            ms.setenv("LEOEC_HOST_BATCH", "0")
+        stats = le._lib._current.leoec_measure_hostq_stats
+    specs = [("vandrs", 10, 4, 8, 1048576), ("vandrs", 10, 4, 8, 1048576),
+             ("vandrs", 10, 4, 8, 300001), ("cauchyrs", 10, 4, 8, 1048576 + 77),
+             ("isars", 10, 4, 8, 65536 + 7), ("liberation", 4, 2, 7, 777777),
+             ("vandrs", 4, 2, 16, 123457), ("vandrs", 6, 3, 32, 99999),
+             ("vandrs", 10, 4, 8, 9 << 20), ("cauchyrs", 4, 2, 3, 5000),
+             ("vandrs", 20, 6, 8, 2000003)]
+    cases = [_capi_case(le, oracle, *sp, seed=100 + i) for i, sp in enumerate(specs)]
+    import ctypes
+    buf = (ctypes.c_double * 14)()
+    if stats:
+        stats(buf)
+
+    def worker(t):
+        for r in range(8):
+            e = _capi_roundtrip(le, cases[(t + r) % len(cases)], t + r)
+            if e:
+                return f"thread {t}: {e}"
+        return None
+
+    with cf.ThreadPoolExecutor(24) as ex:
+        errs = [e for e in ex.map(worker, range(24)) if e]
+    assert not errs, errs
+    if stats:
+        stats(buf)
+        batches, jobs, launches = buf[0], buf[1], buf[2]
+        if form == "always-batch":
+            # 24 x 8 x 3 calls, minus the 9 MiB ones (per-thread path)
+            assert jobs >= 24 * 8 * 3 * 0.8 and batches < jobs and launches > batches, list(buf)
+        else:
+            assert batches == 0, list(buf)

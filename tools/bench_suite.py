@@ -107,6 +107,7 @@ def main():
     args = ap.parse_args()
     import torch
 
+    os.environ.setdefault("LEOEC_LIBRARY", "measure")  # A/B knobs: libleoec_measure.so
     import leo_erasure_amd as le
     torch.cuda.set_device(0)
     assert le.gf_init() == "ok"
@@ -123,10 +124,12 @@ def main():
     for env, label in [({"LEOEC_GFBIT_LW": "1"}, "lane 4 B"), ({"LEOEC_GFBIT_LW": "4"}, "lane 16 B"),
                        ({"LEOEC_BITMATRIX": "1"}, "masked bitmatrix kernel")]:
         os.environ.update(env)
+        le._lib.measure_reload()  # knobs live in the measurement build
         stripe_case(torch, le, "cauchyrs", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], None,
                     "cfg3 variant (%s): cauchyrs(10,4,8) 1 MiB x1024" % label)
         for k in env:
             os.environ.pop(k)
+            le._lib.measure_reload()  # knobs live in the measurement build
     stripe_case(torch, le, "vandrs", 10, 4, 8, 64 * MiB, 16, R, [0, 1, 2, 3], None,
                 "cfg4: vandrs RS(10,4,8) 64 MiB x16 per GPU")
     stripe_case(torch, le, "isars", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], None,

@@ -1,116 +1,163 @@
-"""End-to-end (host memory) encode rates, RS(10,4,8) 1 MiB objects.
+"""End-to-end (host memory) rates, RS(10,4,8) 1 MiB objects.
 
-The reference path starts and ends in host memory (Erlang binaries), so the
-PCIe-inclusive rate is recorded in DESIGN.md (never as the bench value):
+The reference path starts and ends in host memory (Erlang binaries,
+c_src/rscoding.cpp:41,73-81), called once per object from many scheduler
+threads (basho_bench {concurrent, 4}), so the PCIe-inclusive rate is
+recorded in DESIGN.md (never as the bench value):
 
-  nif    leoec_encode() per object from pageable memory (the NIF path:
-         H2D object, kernel, D2H parity, synchronous), 1 thread;
-  pinned batched: pinned host objects -> H2D -> leoec_encode_dev -> D2H
-         parity, chunks of `chunk` objects double-buffered on two streams.
+  C ABI leoec_encode / leoec_decode per object from pageable memory, T
+  concurrent caller threads, under
+    batch       the default: calls that arrive while the GPU is busy are
+                packed into one H2D / launch / D2H (hostq.cpp)
+    per-thread  LEOEC_HOST_BATCH=0: each call its own copies on its
+                thread's stream (the round-1 path)
+  plus the Python mirror (NIF-equivalent term handling) at one caller, and
+  the pinned, batched device-API path (H2D -> leoec_encode_dev -> D2H on two
+  streams) as the link ceiling.
 
-    python tools/e2e_bench.py
+    python tools/e2e_bench.py [--quick]
 """
 import json
 import os
 import sys
+import threading
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+K, M, W, SIZE = 10, 4, 8, 1 << 20
+LOST = [0, 1, 2, 3]
 
-def host_paths(le, K, M, W, size, bs, filled, tag):
-    import threading
+
+def callers(le, T, per, op, bs, filled, tag):
+    """T threads calling leoec_{op} back to back: 3 trials of `per` seconds
+    (after a warm-up trial); the median trial's rate."""
+    import ctypes
 
     import numpy as np
-    # --- NIF path, pageable, one object per call
-    data = np.random.default_rng(1).integers(0, 256, size, dtype=np.uint8).tobytes()
-    for _ in range(3):
-        le.nif_encode("vandrs", (K, M, W), data, size)
-    n = 200
-    t0 = time.perf_counter()
-    for _ in range(n):
-        st, _ = le.nif_encode("vandrs", (K, M, W), data, size)
-        assert st == "ok"
-    t = time.perf_counter() - t0
-    print(json.dumps({"path": f"nif leoec_encode, 1 object/call, 1 thread [{tag}]",
-                      "GiBps": round(n * size / t / 2**30, 2), "us_per_object": round(t / n * 1e6, 1)}))
-
-    # --- NIF decode, data blocks {0,1,2,3} lost (rebuilt on the GPU), 1 thread
-    st, blocks = le.nif_encode("vandrs", (K, M, W), data, size)
-    ids = list(range(4, K + M))
-    surv = [blocks[i] for i in ids]
-    for _ in range(3):
-        le.nif_decode("vandrs", (K, M, W), surv, ids, size)
-    t0 = time.perf_counter()
-    for _ in range(n):
-        st, out = le.nif_decode("vandrs", (K, M, W), surv, ids, size)
-        assert st == "ok"
-    t = time.perf_counter() - t0
-    assert out == data
-    print(json.dumps({"path": f"nif leoec_decode (lose 0-3), 1 object/call, 1 thread [{tag}]",
-                      "GiBps": round(n * size / t / 2**30, 2), "us_per_object": round(t / n * 1e6, 1)}))
-
-    # --- C ABI leoec_encode (host memory), T concurrent callers (dirty schedulers)
     bsz = (K + M - filled) * bs
-    for T in (1, 4, 8, 16):
-        per = 64
-        srcs = [np.random.default_rng(t).integers(0, 256, size, dtype=np.uint8) for t in range(T)]
-        outs = [np.empty(bsz, dtype=np.uint8) for _ in range(T)]
+    rng = np.random.default_rng(T)
+    srcs = [rng.integers(0, 256, SIZE, dtype=np.uint8) for _ in range(T)]
+    outs = [np.empty(bsz, dtype=np.uint8) for _ in range(T)]
+    for t in range(T):
+        assert le.lib.leoec_encode(2, K, M, W, srcs[t].ctypes.data, SIZE, outs[t].ctypes.data, bsz) == 0
+    # decode inputs: blocks 4..13 of each thread's object (pointers into src / out)
+    ids = list(range(4, K + M))
+    ptrs, idv, decs = [], (ctypes.c_int * len(ids))(*ids), []
+    for t in range(T):
+        p = []
+        for i in ids:
+            if i < filled:
+                p.append(srcs[t].ctypes.data + i * bs)
+            else:
+                p.append(outs[t].ctypes.data + (i - filled) * bs)
+        ptrs.append((ctypes.c_void_p * len(ids))(*p))
+        decs.append(np.empty(SIZE, dtype=np.uint8))
 
+    def call(t):
+        if op == "encode":
+            return le.lib.leoec_encode(2, K, M, W, srcs[t].ctypes.data, SIZE, outs[t].ctypes.data, bsz)
+        return le.lib.leoec_decode(2, K, M, W, ptrs[t], idv, len(ids), bs, SIZE, decs[t].ctypes.data)
+
+    errs = []
+    stats = getattr(le._lib._current, "leoec_measure_hostq_stats", None)
+    buf = (ctypes.c_double * 14)()
+
+    def trial():
+        """All T threads call back to back for `per` seconds; calls/s."""
         ready = threading.Barrier(T + 1)
         go = threading.Event()
+        counts = [0] * T
+        box = {}
 
         def work(t):
-            # warm this thread's stream / staging buffers outside the timed region
-            rc = le.lib.leoec_encode(2, K, M, W, srcs[t].ctypes.data, size, outs[t].ctypes.data, bsz)
-            assert rc == 0
+            if call(t) != 0:  # warm this thread outside the timed region
+                errs.append(t)
             ready.wait()
             go.wait()
-            for _ in range(per):
-                rc = le.lib.leoec_encode(2, K, M, W, srcs[t].ctypes.data, size, outs[t].ctypes.data, bsz)
-                assert rc == 0
+            n = 0
+            while time.perf_counter() < box["end"]:
+                if call(t) != 0:
+                    errs.append(t)
+                n += 1
+            counts[t] = n
 
         ths = [threading.Thread(target=work, args=(t,)) for t in range(T)]
         for th in ths:
             th.start()
         ready.wait()
         t0 = time.perf_counter()
+        box["end"] = t0 + per
         go.set()
         for th in ths:
             th.join()
-        t = time.perf_counter() - t0
-        print(json.dumps({"path": f"C ABI leoec_encode, 1 MiB objects, {T} caller threads [{tag}]",
-                          "GiBps": round(T * per * size / t / 2**30, 2),
-                          "us_per_object_per_thread": round(t / per * 1e6, 1)}))
+        return sum(counts), time.perf_counter() - t0
+
+    trial()  # warm-up trial (first use of the queue's slots)
+    if stats:
+        stats(buf)  # reset
+    runs = [trial() for _ in range(3)]
+    assert not errs, errs
+    if op == "decode":
+        for t in range(T):
+            assert np.array_equal(decs[t], srcs[t]), "decode mismatch"
+    rates = sorted(n * SIZE / dt / 2**30 for n, dt in runs)
+    calls = sum(n for n, _ in runs)
+    dt = sum(d for _, d in runs)
+    rec = {"path": f"C ABI leoec_{op}, 1 MiB objects, {T} caller threads [{tag}]",
+           "GiBps": round(rates[1], 2), "GiBps_min_max": [round(rates[0], 2), round(rates[-1], 2)],
+           "us_per_call": round(dt * T / calls * 1e6, 1), "calls": calls}
+    if stats:
+        stats(buf)
+        nb, nj = buf[0], buf[1]
+        if nb:
+            rec["queue"] = {"batches": int(nb), "jobs_per_batch": round(nj / nb, 2),
+                            "launches_per_batch": round(buf[2] / nb, 2),
+                            "us_per_batch": {k: round(buf[i] / nb, 1) for i, k in [
+                                (6, "open_to_close"), (3, "fill_wait"), (4, "issue"),
+                                (5, "gpu_wait"), (7, "done_to_free")]},
+                            "issue_us": {"max": round(buf[10], 1), "h2d": round(buf[11] / nb, 1),
+                                         "launch": round(buf[12] / nb, 1),
+                                         "d2h": round(buf[13] / nb, 1)},
+                            "us_per_job": {"reserve_wait": round(buf[9] / nj, 1),
+                                           "done_wait": round(buf[8] / nj, 1)}}
+    print(json.dumps(rec), flush=True)
+    return rec
 
 
-
-def main():
+def mirror(le, tag):
     import numpy as np
+    data = np.random.default_rng(1).integers(0, 256, SIZE, dtype=np.uint8).tobytes()
+    for _ in range(3):
+        le.nif_encode("vandrs", (K, M, W), data, SIZE)
+    n = 200
+    t0 = time.perf_counter()
+    for _ in range(n):
+        st, blocks = le.nif_encode("vandrs", (K, M, W), data, SIZE)
+        assert st == "ok"
+    t = time.perf_counter() - t0
+    print(json.dumps({"path": f"Python mirror nif_encode, 1 caller [{tag}]",
+                      "GiBps": round(n * SIZE / t / 2**30, 2), "us_per_call": round(t / n * 1e6, 1)}))
+    ids = list(range(4, K + M))
+    surv = [blocks[i] for i in ids]
+    t0 = time.perf_counter()
+    for _ in range(n):
+        st, out = le.nif_decode("vandrs", (K, M, W), surv, ids, SIZE)
+        assert st == "ok"
+    t = time.perf_counter() - t0
+    assert out == data
+    print(json.dumps({"path": f"Python mirror nif_decode (lose 0-3), 1 caller [{tag}]",
+                      "GiBps": round(n * SIZE / t / 2**30, 2), "us_per_call": round(t / n * 1e6, 1)}),
+          flush=True)
+
+
+def pinned_ceiling(le, bs):
     import torch
-
-    import leo_erasure_amd as le
-    torch.cuda.set_device(0)
-    assert le.gf_init() == "ok"
-    K, M, W, size = 10, 4, 8, 1 << 20
-    bs, filled = le.layout("vandrs", (K, M, W), size)
-
-    # Host staging forms of the host entry points (engine.cpp): the pinned
-    # ring at several chunk sizes, and plain pageable copies.
-    forms = [("auto", "256"), ("pageable", "256"), ("gather", "256"), ("pinned", "1024")]
-    if len(sys.argv) > 1 and sys.argv[1] == "--quick":
-        forms = [("auto", "256"), ("pageable", "256")]
-    for staging, ck in forms:
-        os.environ["LEOEC_HOST_STAGING"] = staging
-        os.environ["LEOEC_STAGE_CHUNK_KIB"] = ck
-        host_paths(le, K, M, W, size, bs, filled, f"{staging}/{ck}KiB")
-
-    # --- pinned, batched, two streams
     total, chunk = 1024, 64
-    host = torch.randint(0, 256, (total, size), dtype=torch.uint8).pin_memory()
+    host = torch.randint(0, 256, (total, SIZE), dtype=torch.uint8).pin_memory()
     hpar = torch.empty((total, M * bs), dtype=torch.uint8).pin_memory()
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-    dobj = [torch.empty((chunk, size), dtype=torch.uint8, device="cuda") for _ in streams]
+    dobj = [torch.empty((chunk, SIZE), dtype=torch.uint8, device="cuda") for _ in streams]
     dpar = [torch.empty((chunk, M * bs), dtype=torch.uint8, device="cuda") for _ in streams]
 
     def run():
@@ -118,7 +165,7 @@ def main():
             s = streams[i % 2]
             with torch.cuda.stream(s):
                 dobj[i % 2].copy_(host[c0:c0 + chunk], non_blocking=True)
-                le.device.encode("vandrs", (K, M, W), dobj[i % 2], size, dpar[i % 2],
+                le.device.encode("vandrs", (K, M, W), dobj[i % 2], SIZE, dpar[i % 2],
                                  stream=s.cuda_stream)
                 hpar[c0:c0 + chunk].copy_(dpar[i % 2], non_blocking=True)
         torch.cuda.synchronize()
@@ -129,17 +176,50 @@ def main():
     for _ in range(reps):
         run()
     t = (time.perf_counter() - t0) / reps
-    h2d = total * size
-    d2h = total * M * bs
-    print(json.dumps({"path": "pinned batched H2D+encode+D2H (2 streams, 64-object chunks)",
-                      "GiBps_payload": round(total * size / t / 2**30, 2),
-                      "pcie_GBps": round((h2d + d2h) / t / 1e9, 2), "ms": round(t * 1e3, 2)}))
-    # spot-check one object's parity against a fresh device encode
-    dev = host[:1].cuda()
-    p = torch.empty((1, M * bs), dtype=torch.uint8, device="cuda")
-    le.device.encode("vandrs", (K, M, W), dev, size, p)
-    torch.cuda.synchronize()
-    assert torch.equal(p.cpu(), hpar[:1])
+    print(json.dumps({"path": "pinned batched H2D+encode+D2H (device API, 2 streams, 64-object chunks)",
+                      "GiBps": round(total * SIZE / t / 2**30, 2),
+                      "pcie_GBps": round(total * (SIZE + M * bs) / t / 1e9, 2)}), flush=True)
+
+
+def main():
+    import torch
+
+    os.environ.setdefault("LEOEC_LIBRARY", "measure")  # A/B knobs: libleoec_measure.so
+    import leo_erasure_amd as le
+    torch.cuda.set_device(0)
+    assert le.gf_init() == "ok"
+    bs, filled = le.layout("vandrs", (K, M, W), SIZE)
+    quick = "--quick" in sys.argv
+    if "--queue-ab" in sys.argv:  # batching-queue policies (hostq.cpp knobs)
+        # default: close when the previous H2D is done, poll events, depth 3
+        # default: idle queue -> up to 4 calls direct, else batched; a batch
+        # closes when the previous H2D is done; events polled; depth 3
+        forms = [("default", {}),
+                 ("always-batch", {"LEOEC_HOSTQ_DIRECT": "0", "LEOEC_HOSTQ_DIRECT_MAP": "0"}),
+                 ("direct<=2", {"LEOEC_HOSTQ_DIRECT": "2"}),
+                 ("direct<=8", {"LEOEC_HOSTQ_DIRECT": "8", "LEOEC_HOSTQ_DIRECT_MAP": "8"}),
+                 ("sync-wait", {"LEOEC_HOSTQ_SYNC": "0"}),
+                 ("close-asap", {"LEOEC_HOSTQ_CLOSE": "0"}),
+                 ("depth2", {"LEOEC_HOSTQ_DEPTH": "2"})]
+        threads, with_mirror = (1, 2, 4, 8, 16, 32), False
+    else:
+        forms = [("batch", {}), ("per-thread", {"LEOEC_HOST_BATCH": "0"})]
+        threads, with_mirror = ((1, 8) if quick else (1, 2, 4, 8, 16, 32)), True
+    knobs = {k for _, env in forms for k in env}
+    for tag, env in forms:
+        for k in knobs:
+            os.environ.pop(k, None)
+        os.environ.update(env)
+        le._lib.measure_reload()  # knobs live in the measurement build
+        if with_mirror:
+            mirror(le, tag)
+        for op in ("encode", "decode"):
+            for T in threads:
+                callers(le, T, 0.4, op, bs, filled, tag)
+    for k in knobs:
+        os.environ.pop(k, None)
+    le._lib.measure_reload()
+    pinned_ceiling(le, bs)
 
 
 if __name__ == "__main__":

@@ -37,6 +37,7 @@ def main():
                     help="extra bytes (multiple of 16) per object row beyond max(k, m) * block size")
     args = ap.parse_args()
     import torch
+    os.environ.setdefault("LEOEC_LIBRARY", "measure")  # A/B knobs: libleoec_measure.so
     import leo_erasure_amd as le
     torch.cuda.set_device(0)
     assert le.gf_init() == "ok"
@@ -58,10 +59,12 @@ def main():
     def setenv(v):
         for key in keys:
             os.environ.pop(key, None)
+            le._lib.measure_reload()  # knobs live in the measurement build
         for kv in v.split(","):
             if kv:
                 a, b = kv.split("=")
                 os.environ[a] = b
+                le._lib.measure_reload()  # knobs live in the measurement build
 
     ops = {"encode": (lambda: le.device.encode(args.coding, p, objs, args.size, par),
                       (k + m) * bs * n)}

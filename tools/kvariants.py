@@ -30,6 +30,7 @@ def main():
                     help="launch the reps back to back, synchronise once (bench-like)")
     args = ap.parse_args()
     import torch
+    os.environ.setdefault("LEOEC_LIBRARY", "measure")  # A/B knobs: libleoec_measure.so
     import leo_erasure_amd as le
 
     torch.cuda.set_device(0)
@@ -50,6 +51,7 @@ def main():
     for rnd in range(args.rounds):
         for v in variants:
             os.environ["LEOEC_GF8_VARIANT"] = str(v)
+            le._lib.measure_reload()  # knobs live in the measurement build
             evs = []
             for _ in range(args.reps):
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
@@ -75,6 +77,7 @@ def main():
             torch.cuda.synchronize()
             res["d2d-copy"]["enc"].append(e[0].elapsed_time(e[1]))
     os.environ.pop("LEOEC_GF8_VARIANT", None)
+    le._lib.measure_reload()  # knobs live in the measurement build
     le.device.encode("vandrs", (K, M, W), objs, size, parity)
     le.device.decode("vandrs", (K, M, W), objs, size, parity, [0, 1, 2, 3])
     torch.cuda.synchronize()
