@@ -222,6 +222,7 @@ int gfp_blocks_per_cu() { return knobs().gfp_bpc; }
 int gf8_tile_map() { return knobs().gf8_tmap; }
 int gf8_wg_env() { return knobs().gf8_wg; }
 bool gf8_tile_map_set() { return knobs().gf8_tmap_set; }
+int gf8_tile_group() { return knobs().gf8_tgroup; }
 }  // namespace detail
 
 int launch(const GfApply& p, hipStream_t s) {

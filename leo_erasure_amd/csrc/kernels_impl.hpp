@@ -134,7 +134,9 @@ struct Gf8Args {
   uint32_t nobj;          // objects of the launch
   uint32_t tmap;          // workgroup -> tile order: 0 tile-major, 1 object-major,
                           // 2 tiles of an object visited with stride tperm (coprime),
-                          // 3 xcd_obj_map (shipped for <= kObjMapMaxTiles tiles)
+                          // 3 xcd_obj_map (shipped for <= kObjMapMaxTiles tiles),
+                          // 4 xcd_obj_map over groups of tperm consecutive tiles of
+                          //   the object-major tile order (stripe segments per XCD)
   uint32_t tperm;
 };
 
@@ -430,6 +432,7 @@ gf8_apply(const Gf8Args<K, R> a) {
   if (!PIPE) {
     const uint32_t b = XMAP == 1 ? xcd_group(blockIdx.x, gridDim.x)
                        : (XMAP == 2 || a.tmap == 3) ? xcd_obj_map(blockIdx.x, gridDim.x, a.tiles)
+                       : a.tmap == 4                ? xcd_obj_map(blockIdx.x, gridDim.x, a.tperm)
                                                     : blockIdx.x;
     uint32_t obj, tile;
     if (a.tmap == 1) {
@@ -1474,6 +1477,7 @@ int gfp_blocks_per_cu();  // resident-grid size of gfp_apply (kernels.hip)
 int gf8_tile_map();       // gf8_apply workgroup -> tile order (kernels.hip)
 int gf8_wg_env();         // LEOEC_GF8_WG override of the tile width (kernels.hip)
 bool gf8_tile_map_set();  // LEOEC_GF8_TMAP given (then no automatic xcd_obj_map)
+int gf8_tile_group();     // tiles per XCD group of tile map 4 (kernels.hip)
 // Blocks larger than this run gf8_apply with 64-lane workgroups: 1 MiB objects
 // (bs 104,960) keep 256 lanes, 2 MiB (209,792) and up take 64.
 constexpr uint64_t kGf8NarrowBytes = 160 * 1024;
@@ -1520,6 +1524,7 @@ int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   a.tmap = (uint32_t)gf8_tile_map();
   if (a.tmap == 0 && a.tiles <= kObjMapMaxTiles && !gf8_tile_map_set()) a.tmap = 3;
   a.tperm = 1;
+  if (a.tmap == 4) a.tperm = (uint32_t)(gf8_tile_group() > 0 ? gf8_tile_group() : 64);
   if (a.tmap == 2) {  // stride ~ tiles / 16, coprime with tiles (a bijection on tiles)
     uint32_t q = a.tiles / 16u + 1u;
     auto gcd = [](uint32_t x, uint32_t y) { while (y) { const uint32_t t = x % y; x = y; y = t; } return x; };

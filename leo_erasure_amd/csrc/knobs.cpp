@@ -46,6 +46,7 @@ const Knobs* read_env() {
   k->gf8_tmap = env_int("LEOEC_GF8_TMAP", k->gf8_tmap);
   k->gf8_tmap_set = std::getenv("LEOEC_GF8_TMAP") != nullptr;
   k->gf8_wg = env_int("LEOEC_GF8_WG", k->gf8_wg);
+  k->gf8_tgroup = env_int("LEOEC_GF8_TGROUP", k->gf8_tgroup);
   k->gfw_form = env_int("LEOEC_GFW_FORM", k->gfw_form);
   k->gfp_cpt = env_int("LEOEC_GFP_CPT", k->gfp_cpt);
   k->gfp_bpc = env_int("LEOEC_GFP_BPC", k->gfp_bpc);

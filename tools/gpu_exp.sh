@@ -13,18 +13,24 @@ for p in "${PARTS[@]}"; do
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     suite) step suite 900 python tools/bench_suite.py ${SUITE_ARGS:-} ;;
     e2e) step e2e 600 python tools/e2e_bench.py ;;
+    bench_driver) step bench_driver 600 python bench.py --steps 20 --warmup 5 ;;
+    bench64) step bench64 600 python bench.py --workload 64MiB --no-cpu ;;
+    prof64)
+      cd /tmp && export TMPDIR=/tmp
+      step prof64_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof64_csv" -o run -- python "$ROOT/bench.py" --workload 64MiB --no-cpu
+      cd "$ROOT" ;;
     layout) step layout 600 python tools/layout_exp.py ${LAYOUT_ARGS:-} ;;
     ab) step ab 900 python tools/env_ab.py ${AB_ARGS:-} ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     counters)
       cd /tmp && export TMPDIR=/tmp
       step counters_list 300 rocprofv3 -L
-      step pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_sq" -o run -- python "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu
+      step pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_sq" -o run -- python "$ROOT/bench.py" --steps 3 --warmup 1 --warmup-s 0 --no-cpu
       cd "$ROOT" ;;
     pmc)
       cd /tmp && export TMPDIR=/tmp
-      step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu
-      step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu
+      step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python "$ROOT/bench.py" --steps 3 --warmup 1 --warmup-s 0 --no-cpu
+      step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python "$ROOT/bench.py" --steps 3 --warmup 1 --warmup-s 0 --no-cpu
       step prof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_csv" -o run -- python "$ROOT/bench.py" --no-cpu
       cd "$ROOT" ;;
   esac
