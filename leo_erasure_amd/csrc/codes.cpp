@@ -137,6 +137,16 @@ int vandermonde_coding_matrix(int k, int m, int w, GfMatrix* out) {
 // second row is the published "cbest" list: nonzero elements ordered by the
 // weight of their bitmatrix (ties by value); otherwise cauchy_original
 // (1 / (i xor (m + j))) followed by cauchy_improve_coding_matrix.
+//
+// PARITY UNPINNED for m = 2, w >= 6: Jerasure hard-codes cbest_2 .. cbest_32
+// (cauchy_best_r6.c, not in /root/reference and not fetchable).  The
+// weight-order rule above reproduces the recalled cbest_2 .. cbest_5 tables
+// exactly (tests/test_oracle.py); for w >= 6 it is an extrapolation of that
+// rule, and the cbest length limit of 1023 for w >= 12 is recalled with low
+// confidence.  Round trips and repairs are exact either way (any nonzero
+// second row is MDS with a row of ones); only the parity bytes may differ
+// from the reference's.  No BASELINE config takes this path (DESIGN.md
+// §Oracle, per-class pin table).
 int cauchy_good_coding_matrix(int k, int m, int w, GfMatrix* out) {
   const Field& F = field(w);
   out->rows = m; out->cols = k; out->a.assign((size_t)m * k, 0);
