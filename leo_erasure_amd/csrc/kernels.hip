@@ -37,21 +37,14 @@ ChunkFn gf16_pick(int r, bool acc) {
 #endif  // LEOEC_MEASURE
 
 // Knobs::gfw_form selects the w = 16 / 32 kernel (measurement build):
-//   0 byte-plane v_perm (gfp_apply, shipped)
+//   3 bitsliced planes (gfs_apply, gfs_inst.hip; shipped)
+//   0 byte-plane v_perm (gfp_apply, shipped in round 1)
 //   1 w=16: 2-bit-field v_perm (gf16_apply); w=32: shift-and-add
 //   2 shift-and-add (gfw_apply)
 // Knobs::gfp_cpt = 1|2 sets gfp_apply's 16-byte columns per lane (2 shipped).
+#ifdef LEOEC_MEASURE
 template <int W>
 ChunkFn gfp_pick(int r, bool acc, int cpt) {
-#ifndef LEOEC_MEASURE
-  (void)cpt;
-  static const ChunkFn tbl[2][kMaxR] = {
-      {&launch_gfp_t<W, 1, false, 2>, &launch_gfp_t<W, 2, false, 2>, &launch_gfp_t<W, 3, false, 2>,
-       &launch_gfp_t<W, 4, false, 2>},
-      {&launch_gfp_t<W, 1, true, 2>, &launch_gfp_t<W, 2, true, 2>, &launch_gfp_t<W, 3, true, 2>,
-       &launch_gfp_t<W, 4, true, 2>}};
-  return tbl[acc ? 1 : 0][r - 1];
-#else
   static const ChunkFn tbl[2][2][kMaxR] = {
       {{&launch_gfp_t<W, 1, false, 1>, &launch_gfp_t<W, 2, false, 1>,
         &launch_gfp_t<W, 3, false, 1>, &launch_gfp_t<W, 4, false, 1>},
@@ -62,10 +55,7 @@ ChunkFn gfp_pick(int r, bool acc, int cpt) {
        {&launch_gfp_t<W, 1, true, 2>, &launch_gfp_t<W, 2, true, 2>, &launch_gfp_t<W, 3, true, 2>,
         &launch_gfp_t<W, 4, true, 2>}}};
   return tbl[cpt == 2 ? 1 : 0][acc ? 1 : 0][r - 1];
-#endif
 }
-
-#ifdef LEOEC_MEASURE
 
 template <int W>
 ChunkFn gfw_pick(int r, bool acc) {
@@ -256,11 +246,13 @@ int launch(const GfApply& p, hipStream_t s) {
 #endif
         } else {
           const Knobs& kn = knobs();
-          const int form = kMeasureBuild ? kn.gfw_form : 0;
-          if (form == 0)
+          const int form = kMeasureBuild ? kn.gfw_form : 3;
+          if (form == 3)
+            fn = gfs_pick(p.w, nr, j0 > 0);
+#ifdef LEOEC_MEASURE
+          else if (form == 0)
             fn = p.w == 16 ? gfp_pick<16>(nr, j0 > 0, kn.gfp_cpt)
                            : gfp_pick<32>(nr, j0 > 0, kn.gfp_cpt);
-#ifdef LEOEC_MEASURE
           else if (form == 1 && p.w == 16)
             fn = gf16_pick(nr, j0 > 0);
           else

@@ -1639,5 +1639,8 @@ ChunkFn gf8_launcher(int r, bool acc);
 // Measurement variants of gf8_apply<10, 4> (gf8_exp.hip); nullptr if unknown.
 ChunkFn gf8_variant(int variant);
 
+// Bitsliced GF(2^16) / GF(2^32) launches (gfs_inst.hip), r = 1..kMaxR outputs.
+ChunkFn gfs_pick(int w, int r, bool acc);
+
 }  // namespace detail
 }  // namespace leoec

@@ -33,7 +33,8 @@ struct Knobs {
   bool gf8_tmap_set = false; //   (given: no automatic xcd_obj_map)
   int gf8_wg = 0;            // LEOEC_GF8_WG=64|256: force the gf8 tile width
   int gf8_tgroup = 0;        // LEOEC_GF8_TGROUP: tiles per XCD group of tile map 4
-  int gfw_form = 0;          // LEOEC_GFW_FORM: w=16/32 kernel (0 byte-plane gfp_apply)
+  int gfw_form = 3;          // LEOEC_GFW_FORM: w=16/32 kernel (3 bitsliced gfs_apply,
+                             //   0 byte-plane gfp_apply, 1/2 older forms)
   int gfp_cpt = 2;           // LEOEC_GFP_CPT: gfp_apply 16-byte columns per lane
   int gfp_bpc = 64;          // LEOEC_GFP_BPC: gfp_apply resident blocks per CU
   int bit_form = 4;          // LEOEC_BIT_FORM: bitmatrix kernel form
