@@ -15,11 +15,9 @@
 // into the accumulator: per coefficient and 32 words w/2 * w XORs on
 // average, all full-rate, against 12 (w=32) or 6 (w=16) quarter-rate perms
 // per word for the byte planes.  Bits are taken in pairs (t, t+1), one
-// doubling step computing both x*alpha^t and x*alpha^(t+1); each set bit is
-// its own uniform branch.  (Folding a pair with both bits set into one
-// v_bitop3 per plane made the register allocator keep a copy of the
-// accumulators per branch and copy them back at every merge: 32 v_mov per
-// pair and row, more than the xor3 saves.)
+// doubling step computing both x*alpha^t and x*alpha^(t+1); a pair with both
+// bits set is one v_bitop3 (xor3) per register, so any nonzero pair costs
+// one XOR per plane register (PairMasks).
 //
 // Layout of a lane's words ("rows").  w = 32: rows r[0..31] are the 32
 // words.  w = 16: rows r[0..15] each hold two 16-bit words (low and high
@@ -47,6 +45,14 @@ namespace gfs {
 // Field polynomial taps other than x^0 (gf-complete defaults, as
 // codes.cpp's Field): w = 32: x^32 = x^22 + x^2 + x + 1 (0x400007);
 // w = 16: x^16 = x^12 + x^3 + x + 1 (0x1100B).
+LEOEC_GFS_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+
 template <int W>
 constexpr int tap(int i) {
   return W == 32 ? (i == 0 ? 1 : i == 1 ? 2 : 22) : (i == 0 ? 1 : i == 1 ? 3 : 12);
@@ -83,13 +89,27 @@ LEOEC_GFS_HD void transpose(uint32_t (&r)[W]) {
   swap_stage<W, 1>(r);
 }
 
+// The bit pairs (T, T+1), T even, of a coefficient split three ways, bit T
+// of each mask: both bits set (one v_bitop3 xor3 per register), only bit T,
+// only bit T+1.  Three independent tests, so that every branch updates the
+// accumulators in place (a three-way branch on one value made the compiler
+// give each arm its own destination registers and copy them at the merge).
+struct PairMasks {
+  uint32_t both, lo, hi;
+};
+LEOEC_GFS_HD PairMasks pair_masks(uint32_t c) {
+  constexpr uint32_t kEven = 0x55555555u;
+  return PairMasks{c & (c >> 1) & kEven, c & ~(c >> 1) & kEven, (c >> 1) & ~c & kEven};
+}
+
 // One pair of coefficient bits (T, T+1), then the advance to P_{T+2} and
 // the next pair: template recursion, so that every plane index is a
 // compile-time constant (a runtime index would demote the arrays to scratch
 // memory).  Logical plane k of x * alpha^T lives in pl[(k - T) mod W] (the
 // doubling renames planes; only the tap planes are rewritten).
 template <int W, int R, int T>
-LEOEC_GFS_HD void mac_pair(uint32_t (&pl)[W], uint32_t (&acc)[R][W], const uint32_t (&c)[R]) {
+LEOEC_GFS_HD void mac_pair(uint32_t (&pl)[W], uint32_t (&acc)[R][W], const PairMasks (&c)[R],
+                           uint32_t any) {
   constexpr int M = W - 1;
   // P_{T+1} = P_T * alpha: plane 0 = P_T[W-1], tap planes p = P_T[p-1] ^ P_T[W-1],
   // other planes k = P_T[k-1]
@@ -110,17 +130,22 @@ LEOEC_GFS_HD void mac_pair(uint32_t (&pl)[W], uint32_t (&acc)[R][W], const uint3
   for (int i = 0; i < kTaps; ++i) q1[tap<W>(i)] = tp[i];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const uint32_t two = (c[r] >> T) & 3u;  // wave-uniform: scalar branches
-    if (two & 1u) {
+    // wave-uniform: scalar branches
+    if ((c[r].both >> T) & 1u) {
+#pragma unroll
+      for (int k = 0; k < W; ++k) acc[r][k] = xor3(acc[r][k], q0[k], q1[k]);
+    }
+    if ((c[r].lo >> T) & 1u) {
 #pragma unroll
       for (int k = 0; k < W; ++k) acc[r][k] ^= q0[k];
     }
-    if (two & 2u) {
+    if ((c[r].hi >> T) & 1u) {
 #pragma unroll
       for (int k = 0; k < W; ++k) acc[r][k] ^= q1[k];
     }
   }
   if constexpr (T + 2 < W) {
+    if ((any >> (T + 2)) == 0u) return;  // no coefficient has a higher bit
     // commit P_{T+1}'s tap planes (their registers held P_T[p-1]), advance
     // to P_{T+2}, next pair
 #pragma unroll
@@ -128,14 +153,21 @@ LEOEC_GFS_HD void mac_pair(uint32_t (&pl)[W], uint32_t (&acc)[R][W], const uint3
     const uint32_t top1 = pl[(M - T - 1) & M];  // P_{T+1}[W-1] = P_{T+2}[0]
 #pragma unroll
     for (int i = 0; i < kTaps; ++i) pl[(tap<W>(i) - 2 - T) & M] ^= top1;
-    mac_pair<W, R, T + 2>(pl, acc, c);
+    mac_pair<W, R, T + 2>(pl, acc, c, any);
   }
 }
 
 // acc[r] ^= c[r] * x for R rows, x given as planes pl[] (destroyed).
 template <int W, int R>
 LEOEC_GFS_HD void mac(uint32_t (&pl)[W], uint32_t (&acc)[R][W], const uint32_t (&c)[R]) {
-  mac_pair<W, R, 0>(pl, acc, c);
+  PairMasks m[R];
+  uint32_t any = 0u;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    m[r] = pair_masks(c[r]);
+    any |= c[r];
+  }
+  mac_pair<W, R, 0>(pl, acc, m, any);
 }
 
 // ---------------------------------------------------------------------------
@@ -165,16 +197,20 @@ struct P32Step {
 template <int T>
 LEOEC_GFS_HD P32Step p32_step(const uint32_t (&pl)[16]) {
   P32Step n;
-  n.r0 = swap_halves(pl[(15 - T) & 15]);
-  const uint32_t lo = n.r0 & 0x0000FFFFu, hi = n.r0 << 16;
-  n.r1 = pl[(0 - T) & 15] ^ lo;
-  n.r2 = pl[(1 - T) & 15] ^ lo;
-  n.r6 = pl[(5 - T) & 15] ^ hi;
+  const uint32_t top = pl[(15 - T) & 15];
+  n.r0 = swap_halves(top);
+  // tap terms: new plane 0 (= old plane 31, the high half of `top`) into the
+  // low halves of registers 1 and 2, and into the high half of register 6
+  // (plane 22): one v_bitop3 each, masks in scalar registers
+  n.r1 = pl[(0 - T) & 15] ^ (n.r0 & 0x0000FFFFu);
+  n.r2 = pl[(1 - T) & 15] ^ (n.r0 & 0x0000FFFFu);
+  n.r6 = pl[(5 - T) & 15] ^ (top & 0xFFFF0000u);
   return n;
 }
 
 template <int R, int T>
-LEOEC_GFS_HD void mac_p32_pair(uint32_t (&pl)[16], uint32_t (&acc)[R][16], const uint32_t (&c)[R]) {
+LEOEC_GFS_HD void mac_p32_pair(uint32_t (&pl)[16], uint32_t (&acc)[R][16], const PairMasks (&c)[R],
+                               uint32_t any) {
   const P32Step n = p32_step<T>(pl);
   uint32_t q0[16], q1[16];  // P_T, P_{T+1} (register names)
 #pragma unroll
@@ -188,17 +224,22 @@ LEOEC_GFS_HD void mac_p32_pair(uint32_t (&pl)[16], uint32_t (&acc)[R][16], const
   q1[6] = n.r6;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const uint32_t two = (c[r] >> T) & 3u;  // wave-uniform: scalar branches
-    if (two & 1u) {
+    // wave-uniform: scalar branches
+    if ((c[r].both >> T) & 1u) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[r][i] = xor3(acc[r][i], q0[i], q1[i]);
+    }
+    if ((c[r].lo >> T) & 1u) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[r][i] ^= q0[i];
     }
-    if (two & 2u) {
+    if ((c[r].hi >> T) & 1u) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[r][i] ^= q1[i];
     }
   }
   if constexpr (T + 2 < 32) {
+    if ((any >> (T + 2)) == 0u) return;  // no coefficient has a higher bit
     // commit P_{T+1} (logical register i of P_{T+1} lives in pl[(i - T - 1) mod 16])
     pl[(15 - T) & 15] = n.r0;
     pl[(0 - T) & 15] = n.r1;
@@ -209,7 +250,7 @@ LEOEC_GFS_HD void mac_p32_pair(uint32_t (&pl)[16], uint32_t (&acc)[R][16], const
     pl[(15 - T) & 15] = n2.r1;
     pl[(0 - T) & 15] = n2.r2;
     pl[(4 - T) & 15] = n2.r6;
-    mac_p32_pair<R, T + 2>(pl, acc, c);
+    mac_p32_pair<R, T + 2>(pl, acc, c, any);
   }
 }
 
@@ -217,7 +258,14 @@ LEOEC_GFS_HD void mac_p32_pair(uint32_t (&pl)[16], uint32_t (&acc)[R][16], const
 // (transpose<16> of the 16 words; pl destroyed).
 template <int R>
 LEOEC_GFS_HD void mac_p32(uint32_t (&pl)[16], uint32_t (&acc)[R][16], const uint32_t (&c)[R]) {
-  mac_p32_pair<R, 0>(pl, acc, c);
+  PairMasks m[R];
+  uint32_t any = 0u;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    m[r] = pair_masks(c[r]);
+    any |= c[r];
+  }
+  mac_p32_pair<R, 0>(pl, acc, m, any);
 }
 
 }  // namespace gfs

@@ -19,12 +19,26 @@
 namespace leoec {
 namespace detail {
 
+// One input block of a launch with its column of coefficients: 64 bytes, so
+// that the loop fetches everything it needs for an input with one scalar
+// load, one input ahead (the scalar loads are then waited for behind a whole
+// input's arithmetic instead of in front of it).
+struct GfsCol {
+  const uint8_t* base;
+  uint64_t stride;
+  uint32_t valid;
+  uint32_t pad;
+  uint32_t coef[kMaxR];  // coef[r] = c_rj
+  uint32_t pad2[6];
+};
+static_assert(sizeof(GfsCol) == 64, "GfsCol is one 64-byte scalar load");
+
 template <int R>
 struct GfsArgs {
-  DevShard in[kMaxK];
+  GfsCol col[kMaxK + 1];  // col[K]: empty (valid 0), the target of the last prefetch
+  GfsCol ones;            // a column of 0/1 coefficients done in the word domain (or empty)
   DevShard out[R];
-  uint32_t coef[R][kMaxK];
-  int K;
+  int K;                  // bitsliced columns, >= 1
   uint32_t tiles;  // tiles per object
   uint32_t vmin;   // min valid over all shards of the launch
   uint32_t xmap;   // 1: xcd_obj_map (objects of <= kObjMapMaxTiles tiles)
@@ -36,14 +50,39 @@ constexpr int kGfsRegs = 16;  // registers per value (64 bytes per lane)
 constexpr int kGfsLoads = kGfsRegs / 4;
 constexpr uint32_t kGfsTile = kGfsLanes * 16u * kGfsLoads;
 
-__device__ __forceinline__ void gfs_load(const DevShard& s, uint64_t o, uint32_t t0, bool full,
+// Loads go through a raw buffer resource whose range ends at the shard's
+// valid length rounded up to a 16-byte chunk: a chunk past it reads as zeros
+// without a memory access, so every load is unconditional (no per-lane
+// branch around it, which would make the compiler wait for all outstanding
+// loads, the next input's prefetch included, before each input's arithmetic)
+// and the bytes of the one chunk that straddles `valid` are cleared by
+// gfs_tail() in tiles that are not full.  An input index >= K gets an empty
+// range (col[K], valid 0): the loop's prefetch of "input K" returns zeros.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gfs_rsrc(const uint8_t* base, uint64_t stride,
+                                                           uint32_t valid, uint64_t o) {
+  const uint32_t nrec = valid >= 0xFFFFFFF0u ? 0xFFFFFFF0u : (valid + 15u) & ~15u;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base + o * stride), 0, nrec,
+                                           0x00020000);
+}
+
+__device__ __forceinline__ void gfs_load(__amdgpu_buffer_rsrc_t rs, uint32_t t0,
                                          uint32_t (&rows)[kGfsRegs]) {
-  constexpr int NL = kGfsLoads;
-  const uint8_t* p = s.base + o * s.stride;
 #pragma unroll
-  for (int i = 0; i < NL; ++i) {
+  for (int i = 0; i < kGfsLoads; ++i) {
     const uint32_t off = t0 + (uint32_t)i * (kGfsLanes * 16u) + threadIdx.x * 16u;
-    const u32x4 v = full ? ld16<true>(p + off) : load_guarded(p, off, s.valid);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 2);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rows[4 * i + e] = v[e];
+  }
+}
+
+// Clear the bytes at or past `valid` (tiles that are not full only).
+__device__ __forceinline__ void gfs_tail(uint32_t t0, uint32_t valid, uint32_t (&rows)[kGfsRegs]) {
+#pragma unroll
+  for (int i = 0; i < kGfsLoads; ++i) {
+    const uint32_t off = t0 + (uint32_t)i * (kGfsLanes * 16u) + threadIdx.x * 16u;
+    const uint32_t n = off >= valid ? 0u : (valid - off > 16u ? 16u : valid - off);
+    const u32x4 v = keep_first(u32x4{rows[4 * i], rows[4 * i + 1], rows[4 * i + 2], rows[4 * i + 3]}, n);
 #pragma unroll
     for (int e = 0; e < 4; ++e) rows[4 * i + e] = v[e];
   }
@@ -51,12 +90,13 @@ __device__ __forceinline__ void gfs_load(const DevShard& s, uint64_t o, uint32_t
 
 // Input j (raw words in pl) into the R accumulators.
 template <int W, int R>
-__device__ __forceinline__ void gfs_step(const GfsArgs<R>& a, int j, uint32_t (&pl)[kGfsRegs],
-                                         uint32_t (&acc)[R][kGfsRegs]) {
+__device__ __forceinline__ void gfs_step(const GfsCol& col, uint32_t t0, bool full,
+                                         uint32_t (&pl)[kGfsRegs], uint32_t (&acc)[R][kGfsRegs]) {
+  if (!full) gfs_tail(t0, col.valid, pl);
   gfs::transpose<kGfsRegs>(pl);
   uint32_t c[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) c[r] = a.coef[r][j];
+  for (int r = 0; r < R; ++r) c[r] = col.coef[r];
   if constexpr (W == 32) gfs::mac_p32<R>(pl, acc, c);
   else gfs::mac<16, R>(pl, acc, c);
 }
@@ -75,7 +115,8 @@ gfs_apply(const GfsArgs<R> a) {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (ACC) {
-      gfs_load(a.out[r], o, t0, full, acc[r]);
+      gfs_load(gfs_rsrc(a.out[r].base, a.out[r].stride, a.out[r].valid, o), t0, acc[r]);
+      if (!full) gfs_tail(t0, a.out[r].valid, acc[r]);
       gfs::transpose<kGfsRegs>(acc[r]);
     } else {
 #pragma unroll
@@ -86,17 +127,39 @@ gfs_apply(const GfsArgs<R> a) {
   // transposed and accumulated in place in the other
   const int K = a.K;
   uint32_t bufa[kGfsRegs], bufb[kGfsRegs];
-  gfs_load(a.in[0], o, t0, full, bufa);
-  for (int j = 0; j < K; j += 2) {
-    if (j + 1 < K) gfs_load(a.in[j + 1], o, t0, full, bufb);
-    gfs_step<W, R>(a, j, bufa, acc);
+  GfsCol cur = a.col[0], nx = a.col[K > 1 ? 1 : K];
+  gfs_load(gfs_rsrc(cur.base, cur.stride, cur.valid, o), t0, bufa);
+  for (int j = 0;; j += 2) {
+    gfs_load(gfs_rsrc(nx.base, nx.stride, nx.valid, o), t0, bufb);  // input j+1 (or empty)
+    const GfsCol nx2 = a.col[j + 2 < K ? j + 2 : K];
+    gfs_step<W, R>(cur, t0, full, bufa, acc);
     if (j + 1 >= K) break;
-    if (j + 2 < K) gfs_load(a.in[j + 2], o, t0, full, bufa);
-    gfs_step<W, R>(a, j + 1, bufb, acc);
+    gfs_load(gfs_rsrc(nx2.base, nx2.stride, nx2.valid, o), t0, bufa);  // input j+2 (or empty)
+    const GfsCol nx3 = a.col[j + 3 < K ? j + 3 : K];
+    gfs_step<W, R>(nx, t0, full, bufb, acc);
+    if (j + 2 >= K) break;
+    cur = nx2;
+    nx = nx3;
   }
+  // A column of zeros and ones (encode's column 0) skips the bit domain: it
+  // is XORed into the accumulators after these are transposed back to
+  // words, which saves its transpose and every doubling step.  Its load is
+  // in flight during the transposes; an empty `ones` (no such column) reads
+  // zeros and has no coefficient set.
+  const GfsCol oc = a.ones;
+  uint32_t bufc[kGfsRegs];  // (loading into bufa here put the loop's loads in waterfall loops)
+  gfs_load(gfs_rsrc(oc.base, oc.stride, oc.valid, o), t0, bufc);
+#pragma unroll
+  for (int r = 0; r < R; ++r) gfs::transpose<kGfsRegs>(acc[r]);
+  if (!full) gfs_tail(t0, oc.valid, bufc);
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (oc.coef[r] & 1u) {
+#pragma unroll
+      for (int i = 0; i < kGfsRegs; ++i) acc[r][i] ^= bufc[i];
+    }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    gfs::transpose<kGfsRegs>(acc[r]);
     uint8_t* p = const_cast<uint8_t*>(a.out[r].base) + o * a.out[r].stride;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
@@ -112,16 +175,42 @@ template <int W, int R, bool ACC>
 int launch_gfs_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   GfsArgs<R> a;
   uint32_t vmin = 0xFFFFFFFFu;
-  a.K = c.nk;
-  for (int j = 0; j < kMaxK; ++j) {
-    a.in[j] = j < c.nk ? dev_shard(p.in[c.j0 + j], c.o0) : DevShard{nullptr, 0, 0, 0};
-    if (j < c.nk) vmin = a.in[j].valid < vmin ? a.in[j].valid : vmin;
+  // at most one column whose coefficients are all 0 or 1 goes to `ones`, if
+  // another column remains bitsliced
+  int order[kMaxK], n = 0, ones = -1;
+  for (int j = 0; j < c.nk; ++j) {
+    bool is01 = ones < 0 && c.nk > 1;
+    for (int r = 0; r < R; ++r) is01 = is01 && p.coef[(size_t)(c.r0 + r) * p.K + c.j0 + j] <= 1u;
+    if (is01) ones = j;
+    else order[n++] = j;
+  }
+  a.K = n;
+  auto fill = [&](GfsCol& col, int j) {
+    col = GfsCol{};
+    const DevShard d = dev_shard(p.in[c.j0 + j], c.o0);
+    col.base = d.base;
+    col.stride = d.stride;
+    col.valid = d.valid;
+    vmin = d.valid < vmin ? d.valid : vmin;
+    for (int r = 0; r < R; ++r) col.coef[r] = p.coef[(size_t)(c.r0 + r) * p.K + c.j0 + j];
+  };
+  for (int x = 0; x <= kMaxK; ++x) {
+    if (x < n) {
+      fill(a.col[x], order[x]);
+    } else {
+      a.col[x] = GfsCol{};
+      a.col[x].base = a.col[0].base;  // empty range: never dereferenced
+    }
+  }
+  if (ones >= 0) {
+    fill(a.ones, ones);
+  } else {
+    a.ones = GfsCol{};
+    a.ones.base = a.col[0].base;
   }
   for (int r = 0; r < R; ++r) {
     a.out[r] = dev_shard(p.out[c.r0 + r], c.o0);
     vmin = a.out[r].valid < vmin ? a.out[r].valid : vmin;
-    for (int j = 0; j < kMaxK; ++j)
-      a.coef[r][j] = j < c.nk ? p.coef[(size_t)(c.r0 + r) * p.K + c.j0 + j] : 0u;
   }
   a.tiles = (uint32_t)((p.block_size + kGfsTile - 1) / kGfsTile);
   a.vmin = vmin;

@@ -449,6 +449,11 @@ def test_gfw_kernel_forms_agree(gpu, le, oracle, w, env, measure):
         ids = list(range(1, k + 1))
         st, rep = le.nif_repair("vandrs", (k, m, w), [blocks[i] for i in ids], ids, [0, k + m - 1])
         assert st == "ok" and rep == [blocks[0], blocks[k + m - 1]]
+        # the first parity alone: a row of ones, so every column is 0/1
+        # (gfs_apply's word-domain columns only, no bitsliced input)
+        ids = list(range(k))
+        st, rep = le.nif_repair("vandrs", (k, m, w), [blocks[i] for i in ids], ids, [k])
+        assert st == "ok" and rep == [blocks[k]]
 
 
 def test_device_64MiB_objects(gpu, le, oracle):
