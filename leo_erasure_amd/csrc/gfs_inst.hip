@@ -19,24 +19,10 @@
 namespace leoec {
 namespace detail {
 
-// One input block of a launch with its column of coefficients: 64 bytes, so
-// that the loop fetches everything it needs for an input with one scalar
-// load, one input ahead (the scalar loads are then waited for behind a whole
-// input's arithmetic instead of in front of it).
-struct GfsCol {
-  const uint8_t* base;
-  uint64_t stride;
-  uint32_t valid;
-  uint32_t pad;
-  uint32_t coef[kMaxR];  // coef[r] = c_rj
-  uint32_t pad2[6];
-};
-static_assert(sizeof(GfsCol) == 64, "GfsCol is one 64-byte scalar load");
-
 template <int R>
 struct GfsArgs {
-  GfsCol col[kMaxK + 1];  // col[K]: empty (valid 0), the target of the last prefetch
-  GfsCol ones;            // a column of 0/1 coefficients done in the word domain (or empty)
+  InCol col[kMaxK + 1];  // col[K]: empty (valid 0), the target of the last prefetch
+  InCol ones;            // a column of 0/1 coefficients done in the word domain (or empty)
   DevShard out[R];
   int K;                  // bitsliced columns, >= 1
   uint32_t tiles;  // tiles per object
@@ -50,19 +36,14 @@ constexpr int kGfsRegs = 16;  // registers per value (64 bytes per lane)
 constexpr int kGfsLoads = kGfsRegs / 4;
 constexpr uint32_t kGfsTile = kGfsLanes * 16u * kGfsLoads;
 
-// Loads go through a raw buffer resource whose range ends at the shard's
-// valid length rounded up to a 16-byte chunk: a chunk past it reads as zeros
-// without a memory access, so every load is unconditional (no per-lane
-// branch around it, which would make the compiler wait for all outstanding
-// loads, the next input's prefetch included, before each input's arithmetic)
-// and the bytes of the one chunk that straddles `valid` are cleared by
-// gfs_tail() in tiles that are not full.  An input index >= K gets an empty
-// range (col[K], valid 0): the loop's prefetch of "input K" returns zeros.
+// Loads go through shard_rsrc() (16-byte chunks): every load is
+// unconditional and the bytes of the one chunk that straddles `valid` are
+// cleared by gfs_tail() in tiles that are not full.  An input index >= K gets
+// an empty range (col[K], valid 0): the loop's prefetch of "input K" returns
+// zeros.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t gfs_rsrc(const uint8_t* base, uint64_t stride,
                                                            uint32_t valid, uint64_t o) {
-  const uint32_t nrec = valid >= 0xFFFFFFF0u ? 0xFFFFFFF0u : (valid + 15u) & ~15u;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base + o * stride), 0, nrec,
-                                           0x00020000);
+  return shard_rsrc(base, stride, valid, o, 16u);
 }
 
 __device__ __forceinline__ void gfs_load(__amdgpu_buffer_rsrc_t rs, uint32_t t0,
@@ -90,7 +71,7 @@ __device__ __forceinline__ void gfs_tail(uint32_t t0, uint32_t valid, uint32_t (
 
 // Input j (raw words in pl) into the R accumulators.
 template <int W, int R>
-__device__ __forceinline__ void gfs_step(const GfsCol& col, uint32_t t0, bool full,
+__device__ __forceinline__ void gfs_step(const InCol& col, uint32_t t0, bool full,
                                          uint32_t (&pl)[kGfsRegs], uint32_t (&acc)[R][kGfsRegs]) {
   if (!full) gfs_tail(t0, col.valid, pl);
   gfs::transpose<kGfsRegs>(pl);
@@ -127,15 +108,15 @@ gfs_apply(const GfsArgs<R> a) {
   // transposed and accumulated in place in the other
   const int K = a.K;
   uint32_t bufa[kGfsRegs], bufb[kGfsRegs];
-  GfsCol cur = a.col[0], nx = a.col[K > 1 ? 1 : K];
+  InCol cur = a.col[0], nx = a.col[K > 1 ? 1 : K];
   gfs_load(gfs_rsrc(cur.base, cur.stride, cur.valid, o), t0, bufa);
   for (int j = 0;; j += 2) {
     gfs_load(gfs_rsrc(nx.base, nx.stride, nx.valid, o), t0, bufb);  // input j+1 (or empty)
-    const GfsCol nx2 = a.col[j + 2 < K ? j + 2 : K];
+    const InCol nx2 = a.col[j + 2 < K ? j + 2 : K];
     gfs_step<W, R>(cur, t0, full, bufa, acc);
     if (j + 1 >= K) break;
     gfs_load(gfs_rsrc(nx2.base, nx2.stride, nx2.valid, o), t0, bufa);  // input j+2 (or empty)
-    const GfsCol nx3 = a.col[j + 3 < K ? j + 3 : K];
+    const InCol nx3 = a.col[j + 3 < K ? j + 3 : K];
     gfs_step<W, R>(nx, t0, full, bufb, acc);
     if (j + 2 >= K) break;
     cur = nx2;
@@ -146,7 +127,7 @@ gfs_apply(const GfsArgs<R> a) {
   // words, which saves its transpose and every doubling step.  Its load is
   // in flight during the transposes; an empty `ones` (no such column) reads
   // zeros and has no coefficient set.
-  const GfsCol oc = a.ones;
+  const InCol oc = a.ones;
   uint32_t bufc[kGfsRegs];  // (loading into bufa here put the loop's loads in waterfall loops)
   gfs_load(gfs_rsrc(oc.base, oc.stride, oc.valid, o), t0, bufc);
 #pragma unroll
@@ -185,8 +166,8 @@ int launch_gfs_t(const GfApply& p, const Chunk& c, hipStream_t s) {
     else order[n++] = j;
   }
   a.K = n;
-  auto fill = [&](GfsCol& col, int j) {
-    col = GfsCol{};
+  auto fill = [&](InCol& col, int j) {
+    col = InCol{};
     const DevShard d = dev_shard(p.in[c.j0 + j], c.o0);
     col.base = d.base;
     col.stride = d.stride;
@@ -198,14 +179,14 @@ int launch_gfs_t(const GfApply& p, const Chunk& c, hipStream_t s) {
     if (x < n) {
       fill(a.col[x], order[x]);
     } else {
-      a.col[x] = GfsCol{};
+      a.col[x] = InCol{};
       a.col[x].base = a.col[0].base;  // empty range: never dereferenced
     }
   }
   if (ones >= 0) {
     fill(a.ones, ones);
   } else {
-    a.ones = GfsCol{};
+    a.ones = InCol{};
     a.ones.base = a.col[0].base;
   }
   for (int r = 0; r < R; ++r) {

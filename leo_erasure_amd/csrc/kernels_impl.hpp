@@ -97,6 +97,43 @@ __device__ __forceinline__ u32x4 keep_first(u32x4 v, uint32_t n) {
   return v;
 }
 
+// One input block of a launch with its column of coefficients: 64 bytes, so
+// that a kernel's input loop fetches everything it needs for an input with
+// one scalar load, one input ahead (the scalar loads are then waited for
+// behind a whole input's arithmetic instead of in front of it).  Used by
+// gfs_apply and gfb2_apply.
+struct InCol {
+  const uint8_t* base;
+  uint64_t stride;
+  uint32_t valid;
+  uint32_t pad;
+  uint32_t coef[kMaxR];  // coef[r] = c_rj
+  uint32_t pad2[6];
+};
+static_assert(sizeof(InCol) == 64, "InCol is one 64-byte scalar load");
+
+// Raw buffer resource over one shard of object o whose range ends at `valid`
+// rounded up to a whole chunk of `chunk` bytes (a power of two): loads of
+// chunks past it read as zeros without a memory access, so a kernel's loads
+// can be unconditional (a per-lane branch around a load makes the compiler
+// wait for every outstanding load, prefetches included, at the merge), and
+// the chunk straddling `valid` is cleared by the kernel.  valid 0 = empty.
+// valid <= 2^32 - 16 (launchers refuse blocks of 4 GiB); no clamp, which the
+// compiler would turn into a vector saturating add, making the resource
+// divergent (a waterfall loop around every load).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t shard_rsrc(const uint8_t* base, uint64_t stride,
+                                                             uint32_t valid, uint64_t o,
+                                                             uint32_t chunk) {
+  // the arguments are wave-uniform; readfirstlane says so to the compiler
+  // where a loop-carried copy of one ended up in a VGPR (free for SGPRs)
+  const uint32_t nrec = __builtin_amdgcn_readfirstlane((valid + chunk - 1u) & ~(chunk - 1u));
+  const uint64_t addr = (uint64_t)(uintptr_t)(base + o * stride);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)addr);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>((uintptr_t)(((uint64_t)hi << 32) | lo)), 0, nrec, 0x00020000);
+}
+
 // Guarded load for tiles that cross a block's valid length: a chunk whose
 // first byte is valid is read whole (an aligned 16-byte chunk never crosses a
 // page) and its bytes past `valid` cleared; chunks past `valid` are not read.

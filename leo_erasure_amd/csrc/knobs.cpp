@@ -61,6 +61,7 @@ const Knobs* read_env() {
   k->gfbit_wg = env_int("LEOEC_GFBIT_WG", k->gfbit_wg);
   k->gfbit_ceil = env_int("LEOEC_GFBIT_CEIL", k->gfbit_ceil);
   k->gfbit_lds = env_int("LEOEC_GFBIT_LDS", k->gfbit_lds);
+  k->gfbit_form = env_int("LEOEC_GFBIT_FORM", k->gfbit_form);
   return k;
 }
 
