@@ -33,6 +33,9 @@ ChunkFn gf8_variant(int v) {
     case 32: return &launch_gf8_t<10, 4, false, 1, true, -1, false, false, true, 5, 256, 2, true>; // buffer, auto branchy
     case 33: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 256, 2, false, true>;  // row 0 / column 0 of ones folded
     case 34: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 256, 2>;  // xcd_obj_map always
+    case 35: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 64, 0, true>;  // buffer ld/st wg64, run-time tile map
+    case 36: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 256, 0, false, false, true>;  // loads before LDS staging
+    case 37: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 256, 0, true, false, true>;   // + buffer ld/st
     case 29: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 6, 64>;   // wg64 >=6 waves
     default: return nullptr;
   }

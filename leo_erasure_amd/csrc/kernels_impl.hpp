@@ -437,6 +437,15 @@ __device__ __forceinline__ uint32_t xcd_group(uint32_t b, uint32_t n) {
 // +1-2 % on cauchyrs, +4-8 % on liberation); with many tiles per object
 // (objects of 4 MiB and up) it measured 2-4 % slower than dispatch order.
 constexpr uint32_t kObjMapMaxTiles = 64;
+// Blocks of at least kSegMapMinTiles tiles (64 MiB objects: 6,554 tiles of
+// 1 KiB) run gf8_apply under tile map 4 with groups of kSegMapGroup tiles:
+// XCD x takes every 8th run of 128 consecutive tiles (128 KiB of each block),
+// so each L2 streams whole 128 KiB stretches of the 14 blocks instead of every
+// 8th KiB.  RS(10,4,8) 64 x 64 MiB: 0.723 / 0.726 -> 0.743 / 0.743 of HBM
+// peak (encode / decode, one process, profiles/r02_v13_ab_tmap4_64MiB.log);
+// at 4 MiB (410 tiles) it read 1 % slower, so smaller blocks keep id order.
+constexpr uint32_t kSegMapMinTiles = 4096;
+constexpr uint32_t kSegMapGroup = 128;
 __device__ __forceinline__ uint32_t xcd_obj_map(uint32_t b, uint32_t n, uint32_t tiles) {
   const uint32_t full = (n / tiles / 8u) * 8u * tiles;
   if (b >= full) return b;
@@ -447,8 +456,12 @@ __device__ __forceinline__ uint32_t xcd_obj_map(uint32_t b, uint32_t n, uint32_t
 // One workgroup of WG threads per tile (PIPE = false), or a persistent grid
 // that walks the tiles and issues the loads of its next tile before
 // computing the current one (PIPE = true).
+//  EARLY: the tile's loads are issued before the coefficient tables are
+//         staged into LDS (the staging and its barrier then overlap the
+//         loads' flight instead of delaying them; the barrier waits for LDS
+//         only, never for the loads).
 template <int K, int R, bool ACC, int CPT, bool NT, bool BRANCHY, bool COPY, bool PIPE, bool LDS,
-          int WAVES, int WG, int XMAP, bool BUF = false, bool ONES = false>
+          int WAVES, int WG, int XMAP, bool BUF = false, bool ONES = false, bool EARLY = false>
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 gf8_apply(const Gf8Args<K, R> a) {
   constexpr uint32_t CS = (uint32_t)WG * 16u;  // bytes of one column group
@@ -458,12 +471,16 @@ gf8_apply(const Gf8Args<K, R> a) {
   // large blocks); CPT > 1 forms always launch WG lanes.
   const uint32_t TBr = CPT == 1 ? blockDim.x * 16u : TB;
   __shared__ Gf8Lds<K, R> lds;
-  if (LDS) {
+  auto stage = [&]() {
     for (uint32_t i = threadIdx.x; i < (uint32_t)(R * K); i += blockDim.x) {
       const uint32_t* t = a.tab[i / K][i % K];
       lds.t[i][0] = u32x4{t[0], t[1], t[2], t[3]};
       lds.t[i][1] = u32x4{t[4], 0u, 0u, 0u};
     }
+  };
+  constexpr bool kEarly = EARLY && LDS && !PIPE;
+  if (LDS && !kEarly) {
+    stage();
     __syncthreads();
   }
   if (!PIPE) {
@@ -485,6 +502,11 @@ gf8_apply(const Gf8Args<K, R> a) {
     const bool full = t0 + TBr <= a.vmin;  // wave-uniform
     u32x4 d[CPT][K];
     gf8_load<K, R, CPT, NT, CS, BUF>(a, obj, off, full, d);
+    if (kEarly) {
+      stage();
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: the LDS writes, not the loads
+      __builtin_amdgcn_s_barrier();
+    }
     u32x4 acc[CPT][R];
     gf8_init_store<K, R, ACC, CPT, NT, CS>(a, obj, off, acc);
     if (ONES && LDS && !COPY)
@@ -1524,7 +1546,7 @@ constexpr uint64_t kGf8NarrowBytes = 160 * 1024;
 template <int K, int R, bool ACC, int CPT = kGf8Default.cpt, bool NT = kGf8Default.nt,
           int BRANCHY = kGf8Default.branchy, bool COPY = kGf8Default.copy, bool PIPE = false,
           bool LDS = kGf8Default.lds, int WAVES = kGf8Default.waves, int WG = kThreads,
-          int XMAP = kGf8Default.xmap, bool BUF = false, bool ONES = false>
+          int XMAP = kGf8Default.xmap, bool BUF = false, bool ONES = false, bool EARLY = false>
 int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   Gf8Args<K, R> a;
   a.one = a.zero = 0;
@@ -1559,9 +1581,16 @@ int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   a.total_tiles = (uint32_t)(c.no * a.tiles);
   a.nobj = (uint32_t)c.no;
   a.tmap = (uint32_t)gf8_tile_map();
-  if (a.tmap == 0 && a.tiles <= kObjMapMaxTiles && !gf8_tile_map_set()) a.tmap = 3;
   a.tperm = 1;
-  if (a.tmap == 4) a.tperm = (uint32_t)(gf8_tile_group() > 0 ? gf8_tile_group() : 64);
+  if (a.tmap == 0 && !gf8_tile_map_set()) {  // shipped choice (measure build: unless forced)
+    if (a.tiles <= kObjMapMaxTiles) {
+      a.tmap = 3;
+    } else if (a.tiles >= kSegMapMinTiles) {
+      a.tmap = 4;
+      a.tperm = kSegMapGroup;
+    }
+  }
+  if (a.tmap == 4 && gf8_tile_group() > 0) a.tperm = (uint32_t)gf8_tile_group();
   if (a.tmap == 2) {  // stride ~ tiles / 16, coprime with tiles (a bijection on tiles)
     uint32_t q = a.tiles / 16u + 1u;
     auto gcd = [](uint32_t x, uint32_t y) { while (y) { const uint32_t t = x % y; x = y; y = t; } return x; };
@@ -1583,15 +1612,15 @@ int launch_gf8_t(const GfApply& p, const Chunk& c, hipStream_t s) {
     for (int j = 0; ones && j < K; ++j)
       if ((r == 0 || j == 0) && (p.coef[(size_t)r * p.K + j] & 0xFFu) != 1u) ones = false;
   if (ONES && ones) {
-    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, false, COPY, PIPE, LDS, WAVES, WG, XMAP, BUF, true>),
+    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, false, COPY, PIPE, LDS, WAVES, WG, XMAP, BUF, true, EARLY>),
                        dim3(grid), dim3(wg), 0, s, a);
     return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
   }
   if (branchy)
-    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, true, COPY, PIPE, LDS, WAVES, WG, XMAP, BUF>),
+    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, true, COPY, PIPE, LDS, WAVES, WG, XMAP, BUF, false, EARLY>),
                        dim3(grid), dim3(wg), 0, s, a);
   else
-    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, false, COPY, PIPE, LDS, WAVES, WG, XMAP, BUF>),
+    hipLaunchKernelGGL((gf8_apply<K, R, ACC, CPT, NT, false, COPY, PIPE, LDS, WAVES, WG, XMAP, BUF, false, EARLY>),
                        dim3(grid), dim3(wg), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }

@@ -400,6 +400,35 @@ def test_xcd_object_map_batches(gpu, le, oracle, measure, cls, k, m, w):
         assert outs[0][o, :m * bs].tobytes() == b"".join(r[k:]), f"object {o}"
 
 
+@pytest.mark.parametrize("tgroup", ["5", "128"])
+def test_gf8_segment_map_forms(gpu, le, oracle, measure, tgroup):
+    """gf8 tile map 4 (XCD-interleaved runs of consecutive tiles, shipped for
+    blocks of >= 4096 tiles) forced on smaller objects, with run lengths that
+    straddle object boundaries and a batch whose tail is not a whole group of
+    8 runs: parity identical to tile-major order and to the oracle, and an
+    in-place decode round trip."""
+    k, m, w = 10, 4, 8
+    n, size = 7, 3 * 1048576 + 4321
+    bs, _ = le.layout("vandrs", (k, m, w), size)
+    host, objs = _batch(gpu, n, size, max(k, m) * bs, 77)
+    ref = objs.clone()
+    outs = []
+    measure.setenv("LEOEC_GF8_TGROUP", tgroup)
+    for tmap in ("0", "4"):
+        measure.setenv("LEOEC_GF8_TMAP", tmap)
+        parity = gpu.zeros((n, max(k, m) * bs), dtype=gpu.uint8, device="cuda")
+        le.device.encode("vandrs", (k, m, w), objs, size, parity)
+        objs[:, :4 * bs] = 0xA5
+        le.device.decode("vandrs", (k, m, w), objs, size, parity, [0, 1, 2, 3])
+        gpu.cuda.synchronize()
+        assert gpu.equal(objs, ref), tmap
+        outs.append(parity.cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    for o in (0, n - 1):
+        r = oracle.encode("vandrs", k, m, w, host[o, :size].tobytes())
+        assert outs[1][o, :m * bs].tobytes() == b"".join(r[k:]), f"object {o}"
+
+
 def test_golden_fixtures_gpu(gpu, le):
     """The committed restatement-derived fixtures, through the GPU engine."""
     import json
