@@ -269,9 +269,27 @@ GfbFn pick_r_wg64(int r, bool acc) {
   return tbl[acc ? 1 : 0][r - 1];
 }
 
+// 16-byte lanes in 128-lane workgroups (2 KiB of every packet per tile, as
+// the shipped 8-byte lanes in 256): a wave streams 1 KiB per packet instead
+// of 512 B (tools/packet_ceiling.hip: the pattern reads 0.75-0.78 of peak
+// against 0.66-0.72).
+template <int W, int LW, int PF, int WG>
+GfbFn pick_r_wg(int r, bool acc) {
+  static const GfbFn tbl[2][kMaxR] = {
+      {&launch_gfb_t<W, 1, LW, false, PF, false, 0, WG>, &launch_gfb_t<W, 2, LW, false, PF, false, 0, WG>,
+       &launch_gfb_t<W, 3, LW, false, PF, false, 0, WG>, &launch_gfb_t<W, 4, LW, false, PF, false, 0, WG>},
+      {&launch_gfb_t<W, 1, LW, true, PF, false, 0, WG>, &launch_gfb_t<W, 2, LW, true, PF, false, 0, WG>,
+       &launch_gfb_t<W, 3, LW, true, PF, false, 0, WG>, &launch_gfb_t<W, 4, LW, true, PF, false, 0, WG>}};
+  return tbl[acc ? 1 : 0][r - 1];
+}
+
 GfbFn pick_measure8(int r, bool acc) {
   const Knobs& kn = knobs();
   if (kn.gfbit_wg == 64) return pick_r_wg64<8, 2>(r, acc);
+  // LEOEC_GFBIT_WG=128: 16-byte lanes, next block's loads in flight.  (The
+  // load-then-compute form of this lane width faulted on the GPU in its first
+  // parity run, profiles/r02_v15_cauchy_lw16_pf0_abort.log, and is not built.)
+  if (kn.gfbit_wg == 128) return pick_r_wg<8, 4, 1, 128>(r, acc);
   const int lw = kn.gfbit_lw;
   if (kn.gfbit_ceil && r == 4 && !acc) return &launch_gfb_t<8, 4, 2, false, kPF, true>;
   if (kn.gfbit_xmap == 1 && r == 4 && !acc)

@@ -437,14 +437,16 @@ __device__ __forceinline__ uint32_t xcd_group(uint32_t b, uint32_t n) {
 // +1-2 % on cauchyrs, +4-8 % on liberation); with many tiles per object
 // (objects of 4 MiB and up) it measured 2-4 % slower than dispatch order.
 constexpr uint32_t kObjMapMaxTiles = 64;
-// Blocks of at least kSegMapMinTiles tiles (64 MiB objects: 6,554 tiles of
-// 1 KiB) run gf8_apply under tile map 4 with groups of kSegMapGroup tiles:
-// XCD x takes every 8th run of 128 consecutive tiles (128 KiB of each block),
-// so each L2 streams whole 128 KiB stretches of the 14 blocks instead of every
-// 8th KiB.  RS(10,4,8) 64 x 64 MiB: 0.723 / 0.726 -> 0.743 / 0.743 of HBM
-// peak (encode / decode, one process, profiles/r02_v13_ab_tmap4_64MiB.log);
-// at 4 MiB (410 tiles) it read 1 % slower, so smaller blocks keep id order.
-constexpr uint32_t kSegMapMinTiles = 4096;
+// Blocks of at least kSegMapMinTiles tiles (32 MiB objects: 3,277 tiles of
+// 1 KiB; 64 MiB: 6,554) run gf8_apply under tile map 4 with groups of
+// kSegMapGroup tiles: XCD x takes every 8th run of 128 consecutive tiles
+// (128 KiB of each block), so each L2 streams whole 128 KiB stretches of the
+// 14 blocks instead of every 8th KiB.  RS(10,4,8), one process each
+// (profiles/r02_v13_ab_tmap4_*.log): 64 x 64 MiB 0.720 / 0.734 -> 0.743 /
+// 0.744 of HBM peak (encode / decode), 128 x 32 MiB 0.722 / 0.736 -> 0.743 /
+// 0.742; 16 MiB (1,639 tiles) unchanged and 4 MiB (410 tiles) 1 % slower, so
+// smaller blocks keep id order.
+constexpr uint32_t kSegMapMinTiles = 2048;
 constexpr uint32_t kSegMapGroup = 128;
 __device__ __forceinline__ uint32_t xcd_obj_map(uint32_t b, uint32_t n, uint32_t tiles) {
   const uint32_t full = (n / tiles / 8u) * 8u * tiles;

@@ -45,7 +45,7 @@ struct Knobs {
   int gfbit_xmap = -1;       // LEOEC_GFBIT_XMAP: 0 off, 1 object-contiguous, unset auto
   int gfbit_lw = 2;          // LEOEC_GFBIT_LW: lane width (dwords per packet), w = 8
   int gfbit_pf = 1;          // LEOEC_GFBIT_PF: blocks of load look-ahead, w = 8 (gfbit_apply 0..3; gfb2 0 or 1)
-  int gfbit_wg = 0;          // LEOEC_GFBIT_WG=64: 64-lane workgroups
+  int gfbit_wg = 0;          // LEOEC_GFBIT_WG=64: 64-lane workgroups; 128: 16-byte lanes
   int gfbit_ceil = 0;        // LEOEC_GFBIT_CEIL: traffic-ceiling kernel (not a code)
   int gfbit_lds = 0;         // LEOEC_GFBIT_LDS=1: LDS-staged inputs
   int gfbit_form = 0;        // LEOEC_GFBIT_FORM: 0 gfbit_apply (shipped), 1 gfb2_apply (buffer loads)

@@ -267,7 +267,8 @@ def test_device_roundtrip_bench_shape(gpu, le):
                                  {"LEOEC_BITMATRIX": "1", "LEOEC_BIT_FORM": "2"},
                                  {"LEOEC_GFBIT_FORM": "1"},  # gfb2_apply, next block in flight
                                  {"LEOEC_GFBIT_FORM": "1", "LEOEC_GFBIT_PF": "0"},
-                                 {"LEOEC_GFBIT_FORM": "1", "LEOEC_GFBIT_LW": "1"}],
+                                 {"LEOEC_GFBIT_FORM": "1", "LEOEC_GFBIT_LW": "1"},
+                                 {"LEOEC_GFBIT_WG": "128"}],
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_cauchy_kernel_forms_agree(gpu, le, oracle, env, measure):
     """cauchyrs through the generic masked-bitmatrix kernel and through every
