@@ -77,8 +77,10 @@ def parse(argv=None):
     p.add_argument("--cpu-objects", type=int, default=1024,
                    help="objects in the cpu_baseline sample (copied from rank 0's batch)")
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
-                   help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+    p.add_argument("--traffic", default=",".join(
+        os.path.join(ROOT, "profiles", f) for f in ("pmc_traffic.json", "pmc_traffic_64MiB.json")),
+                   help="PMC-derived HBM bytes per launch, comma-separated files; the one whose "
+                        "objects / object_bytes match the run is used (tools/pmc_traffic.py)")
     return p.parse_args(argv)
 
 
@@ -312,9 +314,11 @@ def run_rank(args, be, rank, world, dist=None):
     enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
     traffic = None
-    if os.path.exists(args.traffic):
+    for tpath in [t for t in args.traffic.split(",") if t]:
+        if traffic is not None or not os.path.exists(tpath):
+            continue
         try:
-            with open(args.traffic) as fh:
+            with open(tpath) as fh:
                 tr = json.load(fh)
             if tr.get("objects") == n and tr.get("object_bytes") == size:
                 traffic = tr.get("encode_bytes_per_launch")

@@ -82,7 +82,11 @@ __device__ __forceinline__ void gfb2_load(__amdgpu_buffer_rsrc_t rs, uint32_t ps
 #pragma unroll
   for (int x = 0; x < W; ++x) {
     const uint32_t vo = off + (uint32_t)x * ps;
-    if constexpr (LW == 2) {
+    if constexpr (LW == 4) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 2);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[x].v[e] = v[e];
+    } else if constexpr (LW == 2) {
       typedef uint32_t v2 __attribute__((ext_vector_type(2)));
       const v2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, vo, 0, 2);
       y[x].v[0] = v[0];
@@ -122,13 +126,13 @@ __device__ __forceinline__ void gfb2_step(uint32_t bs, uint32_t ps, const InCol&
   gfb_accumulate<W, R, LW, false>(acc, y, c);
 }
 
-template <int W, int R, int LW, bool ACC, int PF>
-__global__ void __launch_bounds__(kThreads) gfb2_apply(const Gfb2Args<R> a) {
+template <int W, int R, int LW, bool ACC, int PF, int WG = kThreads>
+__global__ void __launch_bounds__(WG) gfb2_apply(const Gfb2Args<R> a) {
   constexpr uint32_t LB = 4u * LW;
   const uint32_t bid = a.xmap ? xcd_obj_map(blockIdx.x, gridDim.x, a.tiles) : blockIdx.x;
   const uint32_t obj = bid / a.tiles;
   const uint32_t tile = bid - obj * a.tiles;
-  const uint32_t off = tile * (kThreads * LB) + threadIdx.x * LB;
+  const uint32_t off = tile * (WG * LB) + threadIdx.x * LB;
   // lanes past the packet (last tile) compute on whatever they read and do
   // not store: an early return here made the compiler treat the loop's
   // buffer resources as divergent
@@ -193,15 +197,15 @@ __global__ void __launch_bounds__(kThreads) gfb2_apply(const Gfb2Args<R> a) {
   }
 }
 
-template <int W, int R, int LW, bool ACC, int PF>
+template <int W, int R, int LW, bool ACC, int PF, int WG = kThreads>
 int launch_gfb2_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
                   hipStream_t s) {
-  static_assert(LW == 1 || LW == 2, "gfb2_apply lane width");
+  static_assert(LW == 1 || LW == 2 || LW == 4, "gfb2_apply lane width");
   Gfb2Args<R> a;
   a.K = nk;
   a.bs = (uint32_t)p.block_size;
   a.ps = (uint32_t)(p.block_size / (uint64_t)W);
-  constexpr uint32_t tb = kThreads * 4u * LW;
+  constexpr uint32_t tb = WG * 4u * LW;
   a.tiles = (a.ps + tb - 1) / tb;
   for (int x = 0; x <= kMaxK; ++x) {
     InCol& col = a.col[x];
@@ -218,20 +222,20 @@ int launch_gfb2_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint
   }
   for (int i = 0; i < R; ++i) a.out[i] = dev_shard(p.out[r0 + i], o0);
   a.xmap = (a.tiles <= kObjMapMaxTiles && knobs().gfbit_xmap != 0) ? 1u : 0u;
-  hipLaunchKernelGGL((gfb2_apply<W, R, LW, ACC, PF>), dim3((uint32_t)(no * a.tiles)),
-                     dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL((gfb2_apply<W, R, LW, ACC, PF, WG>), dim3((uint32_t)(no * a.tiles)),
+                     dim3(WG), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }
 
 constexpr int kPF2 = 0;  // gfb2_apply: load-then-compute (LEOEC_GFBIT_PF=1: prefetching loop)
 
-template <int W, int LW, int PF = kPF2>
+template <int W, int LW, int PF = kPF2, int WG = kThreads>
 GfbFn pick_r2(int r, bool acc) {
   static const GfbFn tbl[2][kMaxR] = {
-      {&launch_gfb2_t<W, 1, LW, false, PF>, &launch_gfb2_t<W, 2, LW, false, PF>,
-       &launch_gfb2_t<W, 3, LW, false, PF>, &launch_gfb2_t<W, 4, LW, false, PF>},
-      {&launch_gfb2_t<W, 1, LW, true, PF>, &launch_gfb2_t<W, 2, LW, true, PF>,
-       &launch_gfb2_t<W, 3, LW, true, PF>, &launch_gfb2_t<W, 4, LW, true, PF>}};
+      {&launch_gfb2_t<W, 1, LW, false, PF, WG>, &launch_gfb2_t<W, 2, LW, false, PF, WG>,
+       &launch_gfb2_t<W, 3, LW, false, PF, WG>, &launch_gfb2_t<W, 4, LW, false, PF, WG>},
+      {&launch_gfb2_t<W, 1, LW, true, PF, WG>, &launch_gfb2_t<W, 2, LW, true, PF, WG>,
+       &launch_gfb2_t<W, 3, LW, true, PF, WG>, &launch_gfb2_t<W, 4, LW, true, PF, WG>}};
   return tbl[acc ? 1 : 0][r - 1];
 }
 
@@ -349,6 +353,8 @@ GfbFn pick(int w, int r, bool acc, int nk) {
   // LEOEC_GFBIT_FORM=1: gfb2_apply (LEOEC_GFBIT_LW=1: 4 bytes per lane per
   // packet at w = 8; LEOEC_GFBIT_PF=1: its prefetching loop)
   if (knobs().gfbit_form == 1) {
+    // LEOEC_GFBIT_WG=128: 16-byte lanes in 128-lane workgroups, next block in flight
+    if (w == 8 && knobs().gfbit_wg == 128) return pick_r2<8, 4, 1, 128>(r, acc);
     if (w == 8 && knobs().gfbit_lw == 1) return pick_r2<8, 1>(r, acc);
     if (w == 8 && knobs().gfbit_pf == 1) return pick_r2<8, 2, 1>(r, acc);
     return pick2(w, r, acc);
