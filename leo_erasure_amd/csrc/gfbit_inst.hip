@@ -27,7 +27,7 @@ using GfbFn = int (*)(const GfBitApply&, int r0, int j0, int nk, uint64_t o0, ui
                       hipStream_t);
 
 template <int W, int R, int LW, bool ACC, int PF, bool CEIL = false, int KR = 0,
-          int WG = kThreads, int XMAP = 0>
+          int WG = kThreads, int XMAP = 0, int WAVES = 0>
 int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
                  hipStream_t s) {
   GfbArgs<R> a;
@@ -46,7 +46,7 @@ int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint6
   // kObjMapMaxTiles tiles; Knobs::gfbit_xmap = 0 turns it off (A/B)
   a.xmap = (XMAP == 0 && a.tiles <= kObjMapMaxTiles && knobs().gfbit_xmap != 0) ? 1u : 0u;
   if (KR > 0 && nk > KR) return LEOEC_E_ARG;
-  hipLaunchKernelGGL((gfbit_apply<W, R, LW, ACC, PF, CEIL, KR, WG, XMAP>),
+  hipLaunchKernelGGL((gfbit_apply<W, R, LW, ACC, PF, CEIL, KR, WG, XMAP, WAVES>),
                      dim3((uint32_t)(no * a.tiles)), dim3(WG), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }
@@ -287,8 +287,26 @@ GfbFn pick_r_wg(int r, bool acc) {
   return tbl[acc ? 1 : 0][r - 1];
 }
 
+// At least `WAVES` waves per SIMD (the shipped form takes 132 VGPRs: 3).
+template <int W, int LW, int PF, int WAVES>
+GfbFn pick_r_waves(int r, bool acc) {
+  static const GfbFn tbl[2][kMaxR] = {
+      {&launch_gfb_t<W, 1, LW, false, PF, false, 0, kThreads, 0, WAVES>,
+       &launch_gfb_t<W, 2, LW, false, PF, false, 0, kThreads, 0, WAVES>,
+       &launch_gfb_t<W, 3, LW, false, PF, false, 0, kThreads, 0, WAVES>,
+       &launch_gfb_t<W, 4, LW, false, PF, false, 0, kThreads, 0, WAVES>},
+      {&launch_gfb_t<W, 1, LW, true, PF, false, 0, kThreads, 0, WAVES>,
+       &launch_gfb_t<W, 2, LW, true, PF, false, 0, kThreads, 0, WAVES>,
+       &launch_gfb_t<W, 3, LW, true, PF, false, 0, kThreads, 0, WAVES>,
+       &launch_gfb_t<W, 4, LW, true, PF, false, 0, kThreads, 0, WAVES>}};
+  return tbl[acc ? 1 : 0][r - 1];
+}
+
 GfbFn pick_measure8(int r, bool acc) {
   const Knobs& kn = knobs();
+  // LEOEC_GFBIT_WAVES=4|5: the shipped form under a register cap
+  if (kn.gfbit_waves == 4) return pick_r_waves<8, 2, kPF, 4>(r, acc);
+  if (kn.gfbit_waves == 5) return pick_r_waves<8, 2, kPF, 5>(r, acc);
   if (kn.gfbit_wg == 64) return pick_r_wg64<8, 2>(r, acc);
   // LEOEC_GFBIT_WG=128: 16-byte lanes, next block's loads in flight.  (The
   // load-then-compute form of this lane width faulted on the GPU in its first

@@ -32,6 +32,7 @@
 
 #include "../../include/leoec.h"
 #include "kernels.hpp"
+#include "tile_maps.hpp"
 
 namespace leoec {
 namespace detail {
@@ -419,14 +420,9 @@ __device__ __forceinline__ void gf8_store(const Gf8Args<K, R>& a, uint64_t o, ui
 // One workgroup per tile (PIPE = false), or a persistent grid that walks the
 // tiles and issues the loads of its next tile before computing the current
 // one (PIPE = true).
-// Bijective XCD-grouping of workgroup ids (cdna_hip_programming.md T1): the
-// dispatcher deals ids round-robin over the 8 XCDs, so give XCD x the
-// contiguous id range [start(x), start(x+1)).
-__device__ __forceinline__ uint32_t xcd_group(uint32_t b, uint32_t n) {
-  const uint32_t q = n / 8, r = n % 8, x = b % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
-
+// Workgroup-id remaps (xcd_group, xcd_obj_map): tile_maps.hpp, CPU-tested
+// for bijectivity (tests/test_tile_maps.py).
+//
 // Object-interleaved XCD map: with the dispatcher dealing workgroup ids
 // round-robin over the 8 XCDs, give XCD x the objects o = x (mod 8) with all
 // of an object's `tiles` tiles in order, so neighbouring tiles (which share
@@ -448,12 +444,6 @@ constexpr uint32_t kObjMapMaxTiles = 64;
 // smaller blocks keep id order.
 constexpr uint32_t kSegMapMinTiles = 2048;
 constexpr uint32_t kSegMapGroup = 128;
-__device__ __forceinline__ uint32_t xcd_obj_map(uint32_t b, uint32_t n, uint32_t tiles) {
-  const uint32_t full = (n / tiles / 8u) * 8u * tiles;
-  if (b >= full) return b;
-  const uint32_t x = b % 8u, i = b / 8u;
-  return ((i / tiles) * 8u + x) * tiles + i % tiles;
-}
 
 // One workgroup of WG threads per tile (PIPE = false), or a persistent grid
 // that walks the tiles and issues the loads of its next tile before
@@ -1318,9 +1308,12 @@ __device__ __forceinline__ void gfb_accumulate(LaneVec<LW> (&acc)[R][W], LaneVec
 //   PFD > 0: the loads of the next PFD blocks are in flight while block j is
 //            computed (a ring of PFD+1 blocks in VGPRs);
 //   PFD = 0: load block j, then compute on it.
+//   WAVES > 0: ask the register allocator for at least WAVES waves per SIMD
+//            (amdgpu_waves_per_eu; 4 caps the kernel at 128 VGPRs).
 template <int W, int R, int LW, bool ACC, int PFD = 1, bool CEIL = false, int KR = 0,
-          int WG = kThreads, int XMAP = 0>
-__global__ void __launch_bounds__(WG) gfbit_apply(const GfbArgs<R> a) {
+          int WG = kThreads, int XMAP = 0, int WAVES = 0>
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(WAVES > 0 ? WAVES : 1, 8)))
+gfbit_apply(const GfbArgs<R> a) {
   constexpr uint32_t LB = 4u * LW;
   const uint32_t bid = XMAP == 1 ? xcd_group(blockIdx.x, gridDim.x)
                        : (XMAP == 2 || a.xmap) ? xcd_obj_map(blockIdx.x, gridDim.x, a.tiles)

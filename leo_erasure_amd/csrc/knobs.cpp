@@ -62,6 +62,7 @@ const Knobs* read_env() {
   k->gfbit_ceil = env_int("LEOEC_GFBIT_CEIL", k->gfbit_ceil);
   k->gfbit_lds = env_int("LEOEC_GFBIT_LDS", k->gfbit_lds);
   k->gfbit_form = env_int("LEOEC_GFBIT_FORM", k->gfbit_form);
+  k->gfbit_waves = env_int("LEOEC_GFBIT_WAVES", k->gfbit_waves);
   return k;
 }
 

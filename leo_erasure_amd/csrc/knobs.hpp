@@ -48,6 +48,7 @@ struct Knobs {
   int gfbit_wg = 0;          // LEOEC_GFBIT_WG=64: 64-lane workgroups; 128: 16-byte lanes
   int gfbit_ceil = 0;        // LEOEC_GFBIT_CEIL: traffic-ceiling kernel (not a code)
   int gfbit_lds = 0;         // LEOEC_GFBIT_LDS=1: LDS-staged inputs
+  int gfbit_waves = 0;       // LEOEC_GFBIT_WAVES=4|5: register cap (waves per SIMD), w = 8
   int gfbit_form = 0;        // LEOEC_GFBIT_FORM: 0 gfbit_apply (shipped), 1 gfb2_apply (buffer loads)
 };
 
