@@ -239,6 +239,104 @@ GfbFn pick_r2(int r, bool acc) {
   return tbl[acc ? 1 : 0][r - 1];
 }
 
+// gfbx_apply (measurement form, LEOEC_GFBIT_FORM=2; w = 8, 4 output rows,
+// <= 16 inputs): 16-byte lanes without the 16-byte lanes' register bill.  A
+// 128-lane workgroup covers 1 KiB of x in every packet; both waves work on
+// the same 64 columns.  Per input block, wave v loads packets 4v..4v+3
+// (1 KiB contiguous each, raw buffer loads: out-of-range reads return 0) and
+// writes them to LDS; after one barrier each wave reads all 8 packets of its
+// columns back and accumulates output rows 2v, 2v+1 only (acc 2 x 8 x 4 =
+// 64 VGPRs instead of 128).  LDS is double-buffered so the barrier of block
+// j also retires every read of block j-1's buffer, and block j+1's loads are
+// in flight while block j is computed.
+constexpr int kGfbxLanes = 64;                     // columns per workgroup
+constexpr uint32_t kGfbxSlice = kGfbxLanes * 16u;  // bytes of x per tile
+
+template <int W>
+__global__ void __launch_bounds__(2 * kGfbxLanes) gfbx_apply(const GfbArgs<4> a) {
+  static_assert(W % 2 == 0, "two waves split the packets");
+  constexpr int HP = W / 2;  // packets loaded per wave
+  __shared__ u32x4 lds[2][W][kGfbxLanes];
+  const uint32_t lane = threadIdx.x % kGfbxLanes;
+  const uint32_t v = __builtin_amdgcn_readfirstlane(threadIdx.x / kGfbxLanes);
+  const uint32_t bid = a.xmap ? xcd_obj_map(blockIdx.x, gridDim.x, a.tiles) : blockIdx.x;
+  const uint32_t obj = bid / a.tiles;
+  const uint32_t tile = bid - obj * a.tiles;
+  const uint32_t off = tile * kGfbxSlice + lane * 16u;
+  const bool live = off < a.ps;
+  const uint64_t o64 = obj;
+  const int K = a.K;
+  u32x4 p[HP];
+  auto load = [&](int j) {
+    const DevShard d = a.in[j];
+    const auto rs = shard_rsrc(d.base, d.stride, d.valid, o64, 16u);
+#pragma unroll
+    for (int h = 0; h < HP; ++h) {
+      const uint32_t x = v * HP + h;
+      const uint32_t at = x * a.ps + off;
+      u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rs, at, 0, 2);
+      if (d.valid < at + 16u) t = keep_first(t, d.valid > at ? d.valid - at : 0u);
+      p[h] = t;
+    }
+  };
+  LaneVec<4> acc[2][W];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int x = 0; x < W; ++x)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[i][x].v[e] = 0u;
+  load(0);
+  for (int j = 0; j < K; ++j) {
+    const int b = j & 1;
+#pragma unroll
+    for (int h = 0; h < HP; ++h) lds[b][v * HP + h][lane] = p[h];
+    __syncthreads();
+    if (j + 1 < K) load(j + 1);
+    LaneVec<4> y[W];
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const u32x4 t = lds[b][x][lane];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[x].v[e] = t[e];
+    }
+    uint32_t c[2];
+    c[0] = a.coef[2 * v][j];
+    c[1] = a.coef[2 * v + 1][j];
+    gfb_accumulate<W, 2, 4, false>(acc, y, c);
+  }
+  if (!live) return;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const DevShard d = a.out[2 * v + i];
+    uint8_t* q = const_cast<uint8_t*>(d.base) + o64 * d.stride;
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const uint32_t pk = (uint32_t)x * a.ps;
+      lv_store<4>(q + pk, off, d.valid > pk ? d.valid - pk : 0u, acc[i][x]);
+    }
+  }
+}
+
+int launch_gfbx_8(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
+                  hipStream_t s) {
+  GfbArgs<4> a;
+  a.K = nk;
+  a.ps = (uint32_t)(p.block_size / 8u);
+  a.tiles = (a.ps + kGfbxSlice - 1) / kGfbxSlice;
+  for (int j = 0; j < kMaxK; ++j)
+    a.in[j] = j < nk ? dev_shard(p.in[j0 + j], o0) : DevShard{nullptr, 0, 0, 0};
+  for (int i = 0; i < 4; ++i) {
+    a.out[i] = dev_shard(p.out[r0 + i], o0);
+    for (int j = 0; j < kMaxK; ++j)
+      a.coef[i][j] = j < nk ? p.coef[(size_t)(r0 + i) * p.K + j0 + j] : 0u;
+  }
+  a.xmap = (a.tiles <= kObjMapMaxTiles && knobs().gfbit_xmap != 0) ? 1u : 0u;
+  hipLaunchKernelGGL((gfbx_apply<8>), dim3((uint32_t)(no * a.tiles)), dim3(2 * kGfbxLanes), 0, s,
+                     a);
+  return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
+}
+
 template <int W, int R, bool ACC>
 int launch_gfb_lds_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
                      hipStream_t s) {
@@ -370,6 +468,10 @@ GfbFn pick(int w, int r, bool acc, int nk) {
 #ifdef LEOEC_MEASURE
   // LEOEC_GFBIT_FORM=1: gfb2_apply (LEOEC_GFBIT_LW=1: 4 bytes per lane per
   // packet at w = 8; LEOEC_GFBIT_PF=1: its prefetching loop)
+  // LEOEC_GFBIT_FORM=2: gfbx_apply where it applies (w = 8, 4 rows, one input
+  // chunk, no accumulation), the shipped kernel otherwise
+  if (knobs().gfbit_form == 2 && w == 8 && r == 4 && !acc && nk <= kMaxK)
+    return &launch_gfbx_8;
   if (knobs().gfbit_form == 1) {
     // LEOEC_GFBIT_WG=128: 16-byte lanes in 128-lane workgroups, next block in flight
     if (w == 8 && knobs().gfbit_wg == 128) return pick_r2<8, 4, 1, 128>(r, acc);

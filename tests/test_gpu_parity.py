@@ -270,7 +270,8 @@ def test_device_roundtrip_bench_shape(gpu, le):
                                  {"LEOEC_GFBIT_FORM": "1", "LEOEC_GFBIT_LW": "1"},
                                  {"LEOEC_GFBIT_WG": "128"},
                                  {"LEOEC_GFBIT_FORM": "1", "LEOEC_GFBIT_WG": "128"},
-                                 {"LEOEC_GFBIT_WAVES": "4"}, {"LEOEC_GFBIT_WAVES": "5"}],
+                                 {"LEOEC_GFBIT_WAVES": "4"}, {"LEOEC_GFBIT_WAVES": "5"},
+                                 {"LEOEC_GFBIT_FORM": "2"}],  # gfbx_apply (LDS-shared, split rows)
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_cauchy_kernel_forms_agree(gpu, le, oracle, env, measure):
     """cauchyrs through the generic masked-bitmatrix kernel and through every
