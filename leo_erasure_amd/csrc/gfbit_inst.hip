@@ -14,8 +14,7 @@
 // flight at 184 VGPRs, against 0.711 / 0.703), so it stays an A/B form.
 #include <utility>
 
-#include "kernels_impl.hpp"
-#include "knobs.hpp"
+#include "gfbit_impl.hpp"
 
 namespace leoec {
 
@@ -23,222 +22,9 @@ using namespace detail;
 
 namespace {
 
-using GfbFn = int (*)(const GfBitApply&, int r0, int j0, int nk, uint64_t o0, uint64_t no,
-                      hipStream_t);
-
-template <int W, int R, int LW, bool ACC, int PF, bool CEIL = false, int KR = 0,
-          int WG = kThreads, int XMAP = 0, int WAVES = 0>
-int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
-                 hipStream_t s) {
-  GfbArgs<R> a;
-  a.K = nk;
-  a.ps = (uint32_t)(p.block_size / (uint64_t)W);
-  constexpr uint32_t tb = WG * 4u * LW;
-  a.tiles = (a.ps + tb - 1) / tb;
-  for (int j = 0; j < kMaxK; ++j)
-    a.in[j] = j < nk ? dev_shard(p.in[j0 + j], o0) : DevShard{nullptr, 0, 0, 0};
-  for (int i = 0; i < R; ++i) {
-    a.out[i] = dev_shard(p.out[r0 + i], o0);
-    for (int j = 0; j < kMaxK; ++j)
-      a.coef[i][j] = j < nk ? p.coef[(size_t)(r0 + i) * p.K + j0 + j] : 0u;
-  }
-  // objects interleaved over the XCDs (xcd_obj_map) for objects of at most
-  // kObjMapMaxTiles tiles; Knobs::gfbit_xmap = 0 turns it off (A/B)
-  a.xmap = (XMAP == 0 && a.tiles <= kObjMapMaxTiles && knobs().gfbit_xmap != 0) ? 1u : 0u;
-  if (KR > 0 && nk > KR) return LEOEC_E_ARG;
-  hipLaunchKernelGGL((gfbit_apply<W, R, LW, ACC, PF, CEIL, KR, WG, XMAP, WAVES>),
-                     dim3((uint32_t)(no * a.tiles)), dim3(WG), 0, s, a);
-  return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
-}
-
-constexpr int kPF = 1;  // gfbit_apply: blocks of load look-ahead
-
-template <int W, int LW, int PF = kPF>
-GfbFn pick_r(int r, bool acc) {
-  static const GfbFn tbl[2][kMaxR] = {
-      {&launch_gfb_t<W, 1, LW, false, PF>, &launch_gfb_t<W, 2, LW, false, PF>,
-       &launch_gfb_t<W, 3, LW, false, PF>, &launch_gfb_t<W, 4, LW, false, PF>},
-      {&launch_gfb_t<W, 1, LW, true, PF>, &launch_gfb_t<W, 2, LW, true, PF>,
-       &launch_gfb_t<W, 3, LW, true, PF>, &launch_gfb_t<W, 4, LW, true, PF>}};
-  return tbl[acc ? 1 : 0][r - 1];
-}
+using namespace gfbit_detail;
 
 #ifdef LEOEC_MEASURE
-template <int R>
-struct Gfb2Args {
-  InCol col[kMaxK + 1];  // col[K]: empty (valid 0), the target of the last prefetch
-  DevShard out[R];
-  int K;
-  uint32_t ps;     // packet bytes
-  uint32_t bs;     // block bytes (w packets)
-  uint32_t tiles;  // tiles per object (over one packet)
-  uint32_t xmap;   // 1: xcd_obj_map
-};
-
-// Packet x of the block behind rs: this lane's 4*LW bytes at off.
-template <int W, int LW>
-__device__ __forceinline__ void gfb2_load(__amdgpu_buffer_rsrc_t rs, uint32_t ps, uint32_t off,
-                                          LaneVec<LW> (&y)[W]) {
-#pragma unroll
-  for (int x = 0; x < W; ++x) {
-    const uint32_t vo = off + (uint32_t)x * ps;
-    if constexpr (LW == 4) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 2);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) y[x].v[e] = v[e];
-    } else if constexpr (LW == 2) {
-      typedef uint32_t v2 __attribute__((ext_vector_type(2)));
-      const v2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, vo, 0, 2);
-      y[x].v[0] = v[0];
-      y[x].v[LW - 1] = v[1];
-    } else {
-      y[x].v[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 0, 2);
-    }
-  }
-}
-
-// Bytes at or past the block's valid length cleared (blocks shorter than bs).
-template <int W, int LW>
-__device__ __forceinline__ void gfb2_tail(uint32_t valid, uint32_t ps, uint32_t off,
-                                          LaneVec<LW> (&y)[W]) {
-#pragma unroll
-  for (int x = 0; x < W; ++x) {
-    const uint32_t p = off + (uint32_t)x * ps;
-    const uint32_t n = p >= valid ? 0u : (valid - p > 4u * LW ? 4u * LW : valid - p);
-#pragma unroll
-    for (int e = 0; e < LW; ++e) {
-      const uint32_t lo = 4u * e;
-      y[x].v[e] &= n >= lo + 4u ? 0xFFFFFFFFu : (n <= lo ? 0u : (1u << (8u * (n - lo))) - 1u);
-    }
-  }
-}
-
-// (takes no reference to the kernel argument block: one would make the
-// compiler read the arguments through vector loads, and the buffer resources
-// built from them divergent)
-template <int W, int R, int LW>
-__device__ __forceinline__ void gfb2_step(uint32_t bs, uint32_t ps, const InCol& col, uint32_t off,
-                                          LaneVec<LW> (&y)[W], LaneVec<LW> (&acc)[R][W]) {
-  if (col.valid < bs) gfb2_tail<W, LW>(col.valid, ps, off, y);
-  uint32_t c[R];
-#pragma unroll
-  for (int i = 0; i < R; ++i) c[i] = col.coef[i];
-  gfb_accumulate<W, R, LW, false>(acc, y, c);
-}
-
-template <int W, int R, int LW, bool ACC, int PF, int WG = kThreads>
-__global__ void __launch_bounds__(WG) gfb2_apply(const Gfb2Args<R> a) {
-  constexpr uint32_t LB = 4u * LW;
-  const uint32_t bid = a.xmap ? xcd_obj_map(blockIdx.x, gridDim.x, a.tiles) : blockIdx.x;
-  const uint32_t obj = bid / a.tiles;
-  const uint32_t tile = bid - obj * a.tiles;
-  const uint32_t off = tile * (WG * LB) + threadIdx.x * LB;
-  // lanes past the packet (last tile) compute on whatever they read and do
-  // not store: an early return here made the compiler treat the loop's
-  // buffer resources as divergent
-  const bool live = off < a.ps;
-  const uint64_t o64 = obj;
-  LaneVec<LW> acc[R][W];
-#pragma unroll
-  for (int i = 0; i < R; ++i)
-#pragma unroll
-    for (int x = 0; x < W; ++x) {
-      if (ACC && live) {
-        const uint32_t pk = (uint32_t)x * a.ps;
-        const uint32_t bv = a.out[i].valid;
-        acc[i][x] = lv_load<LW>(a.out[i].base + o64 * a.out[i].stride + pk, off,
-                                bv > pk ? bv - pk : 0u);
-      } else {
-#pragma unroll
-        for (int e = 0; e < LW; ++e) acc[i][x].v[e] = 0u;
-      }
-    }
-  const int K = a.K;
-  if constexpr (PF == 0) {
-    // load, then compute: no second buffer (the prefetching loop below
-    // needs ~64 more VGPRs, i.e. 2 waves per SIMD instead of 4)
-    LaneVec<LW> y[W];
-    InCol cur = a.col[0];
-    for (int j = 0; j < K; ++j) {
-      gfb2_load<W, LW>(shard_rsrc(cur.base, cur.stride, cur.valid, o64, LB), a.ps, off, y);
-      const InCol nx = a.col[j + 1];  // col[K] is the empty record
-      gfb2_step<W, R, LW>(a.bs, a.ps, cur, off, y, acc);
-      cur = nx;
-    }
-  } else {
-    LaneVec<LW> ya[W], yb[W];
-    InCol cur = a.col[0], nx = a.col[K > 1 ? 1 : K];
-    gfb2_load<W, LW>(shard_rsrc(cur.base, cur.stride, cur.valid, o64, LB), a.ps, off, ya);
-    for (int j = 0;; j += 2) {
-      gfb2_load<W, LW>(shard_rsrc(nx.base, nx.stride, nx.valid, o64, LB), a.ps, off, yb);
-      const InCol nx2 = a.col[j + 2 < K ? j + 2 : K];
-      gfb2_step<W, R, LW>(a.bs, a.ps, cur, off, ya, acc);
-      __builtin_amdgcn_sched_barrier(0);  // keep the next loads below: same registers
-      if (j + 1 >= K) break;
-      gfb2_load<W, LW>(shard_rsrc(nx2.base, nx2.stride, nx2.valid, o64, LB), a.ps, off, ya);
-      const InCol nx3 = a.col[j + 3 < K ? j + 3 : K];
-      gfb2_step<W, R, LW>(a.bs, a.ps, nx, off, yb, acc);
-      __builtin_amdgcn_sched_barrier(0);
-      if (j + 2 >= K) break;
-      cur = nx2;
-      nx = nx3;
-    }
-  }
-  if (!live) return;
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    uint8_t* p = const_cast<uint8_t*>(a.out[i].base) + o64 * a.out[i].stride;
-    const uint32_t bv = a.out[i].valid;
-#pragma unroll
-    for (int x = 0; x < W; ++x) {
-      const uint32_t pk = (uint32_t)x * a.ps;
-      lv_store<LW>(p + pk, off, bv > pk ? bv - pk : 0u, acc[i][x]);
-    }
-  }
-}
-
-template <int W, int R, int LW, bool ACC, int PF, int WG = kThreads>
-int launch_gfb2_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
-                  hipStream_t s) {
-  static_assert(LW == 1 || LW == 2 || LW == 4, "gfb2_apply lane width");
-  Gfb2Args<R> a;
-  a.K = nk;
-  a.bs = (uint32_t)p.block_size;
-  a.ps = (uint32_t)(p.block_size / (uint64_t)W);
-  constexpr uint32_t tb = WG * 4u * LW;
-  a.tiles = (a.ps + tb - 1) / tb;
-  for (int x = 0; x <= kMaxK; ++x) {
-    InCol& col = a.col[x];
-    col = InCol{};
-    if (x < nk) {
-      const DevShard d = dev_shard(p.in[j0 + x], o0);
-      col.base = d.base;
-      col.stride = d.stride;
-      col.valid = d.valid;
-      for (int i = 0; i < R; ++i) col.coef[i] = p.coef[(size_t)(r0 + i) * p.K + j0 + x];
-    } else {
-      col.base = a.col[0].base;  // empty range: never dereferenced
-    }
-  }
-  for (int i = 0; i < R; ++i) a.out[i] = dev_shard(p.out[r0 + i], o0);
-  a.xmap = (a.tiles <= kObjMapMaxTiles && knobs().gfbit_xmap != 0) ? 1u : 0u;
-  hipLaunchKernelGGL((gfb2_apply<W, R, LW, ACC, PF, WG>), dim3((uint32_t)(no * a.tiles)),
-                     dim3(WG), 0, s, a);
-  return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
-}
-
-constexpr int kPF2 = 0;  // gfb2_apply: load-then-compute (LEOEC_GFBIT_PF=1: prefetching loop)
-
-template <int W, int LW, int PF = kPF2, int WG = kThreads>
-GfbFn pick_r2(int r, bool acc) {
-  static const GfbFn tbl[2][kMaxR] = {
-      {&launch_gfb2_t<W, 1, LW, false, PF, WG>, &launch_gfb2_t<W, 2, LW, false, PF, WG>,
-       &launch_gfb2_t<W, 3, LW, false, PF, WG>, &launch_gfb2_t<W, 4, LW, false, PF, WG>},
-      {&launch_gfb2_t<W, 1, LW, true, PF, WG>, &launch_gfb2_t<W, 2, LW, true, PF, WG>,
-       &launch_gfb2_t<W, 3, LW, true, PF, WG>, &launch_gfb2_t<W, 4, LW, true, PF, WG>}};
-  return tbl[acc ? 1 : 0][r - 1];
-}
-
 // gfbx_apply (measurement form, LEOEC_GFBIT_FORM=2; w = 8, 4 output rows,
 // <= 16 inputs): 16-byte lanes without the 16-byte lanes' register bill.  A
 // 128-lane workgroup covers 1 KiB of x in every packet; both waves work on
@@ -443,21 +229,21 @@ GfbFn pick_measure8(int r, bool acc) {
 
 GfbFn pick2(int w, int r, bool acc) {
   switch (w) {
-    case 8: return pick_r2<8, 2>(r, acc);
-    case 2: return pick_r2<2, 2>(r, acc);
-    case 3: return pick_r2<3, 2>(r, acc);
-    case 4: return pick_r2<4, 2>(r, acc);
-    case 5: return pick_r2<5, 2>(r, acc);
-    case 6: return pick_r2<6, 2>(r, acc);
-    case 7: return pick_r2<7, 2>(r, acc);
-    case 9: return pick_r2<9, 2>(r, acc);
-    case 10: return pick_r2<10, 2>(r, acc);
-    case 11: return pick_r2<11, 2>(r, acc);
-    case 12: return pick_r2<12, 1>(r, acc);
-    case 13: return pick_r2<13, 1>(r, acc);
-    case 14: return pick_r2<14, 1>(r, acc);
-    case 15: return pick_r2<15, 1>(r, acc);
-    case 16: return pick_r2<16, 1>(r, acc);
+    case 8: return measure2<8>(r, acc);
+    case 2: return measure2<2>(r, acc);
+    case 3: return measure2<3>(r, acc);
+    case 4: return measure2<4>(r, acc);
+    case 5: return measure2<5>(r, acc);
+    case 6: return measure2<6>(r, acc);
+    case 7: return measure2<7>(r, acc);
+    case 9: return measure2<9>(r, acc);
+    case 10: return measure2<10>(r, acc);
+    case 11: return measure2<11>(r, acc);
+    case 12: return measure2<12>(r, acc);
+    case 13: return measure2<13>(r, acc);
+    case 14: return measure2<14>(r, acc);
+    case 15: return measure2<15>(r, acc);
+    case 16: return measure2<16>(r, acc);
     default: return nullptr;
   }
 }
@@ -482,21 +268,21 @@ GfbFn pick(int w, int r, bool acc, int nk) {
   if (w == 8) return pick_measure8(r, acc);
 #endif
   switch (w) {
-    case 8: return pick_r<8, 2>(r, acc);
-    case 2: return pick_r<2, 2>(r, acc);
-    case 3: return pick_r<3, 2>(r, acc);
-    case 4: return pick_r<4, 2>(r, acc);
-    case 5: return pick_r<5, 2>(r, acc);
-    case 6: return pick_r<6, 2>(r, acc);
-    case 7: return pick_r<7, 2>(r, acc);
-    case 9: return pick_r<9, 2>(r, acc);
-    case 10: return pick_r<10, 2>(r, acc);
-    case 11: return pick_r<11, 2>(r, acc);
-    case 12: return pick_r<12, 1>(r, acc);
-    case 13: return pick_r<13, 1>(r, acc);
-    case 14: return pick_r<14, 1>(r, acc);
-    case 15: return pick_r<15, 1>(r, acc);
-    case 16: return pick_r<16, 1>(r, acc);
+    case 8: return shipped<8>(r, acc);
+    case 2: return shipped<2>(r, acc);
+    case 3: return shipped<3>(r, acc);
+    case 4: return shipped<4>(r, acc);
+    case 5: return shipped<5>(r, acc);
+    case 6: return shipped<6>(r, acc);
+    case 7: return shipped<7>(r, acc);
+    case 9: return shipped<9>(r, acc);
+    case 10: return shipped<10>(r, acc);
+    case 11: return shipped<11>(r, acc);
+    case 12: return shipped<12>(r, acc);
+    case 13: return shipped<13>(r, acc);
+    case 14: return shipped<14>(r, acc);
+    case 15: return shipped<15>(r, acc);
+    case 16: return shipped<16>(r, acc);
     default: return nullptr;
   }
 }

@@ -1698,7 +1698,10 @@ template <int K>
 ChunkFn gf8_launcher(int r, bool acc);
 
 // Measurement variants of gf8_apply<10, 4> (gf8_exp.hip); nullptr if unknown.
+// gf8_variant_part<P> holds the variants n with n % 4 == P (one TU each).
 ChunkFn gf8_variant(int variant);
+template <int P>
+ChunkFn gf8_variant_part(int variant);
 
 // Bitsliced GF(2^16) / GF(2^32) launches (gfs_inst.hip), r = 1..kMaxR outputs.
 ChunkFn gfs_pick(int w, int r, bool acc);
