@@ -141,15 +141,27 @@ bool is_liberation_encode(const BitApply& p) {
 // Knobs::lib_la = 2|4|8 sets lib_apply's packet look-ahead (measurement
 // build; shipped 2: profiles/r01_v13_ab_lib_la.log, best or within 1 % of
 // best for w = 5..13).
+// lib_apply runs 64-lane workgroups (1 KiB of every packet per tile):
+// liberation 1 MiB encode (7,2,7) 0.682 -> 0.686, (10,2,11) 0.694 -> 0.700,
+// (4,2,7) 0.662 -> 0.689 against 256 lanes (profiles/r02_v22_ab_lib_wg_*.log).
+// Knobs::lib_wg = 256 (measurement build) restores the 256-lane form, which
+// the look-ahead variants (lib_la 4 / 8) also use.
 using LibFn = void (*)(const detail::LibArgs);
+constexpr uint32_t kLibLanes = 64;
+uint32_t lib_lanes() {
+  if (!kMeasureBuild) return kLibLanes;
+  const Knobs& k = knobs();
+  return (k.lib_wg == 256 || k.lib_la != 2) ? (uint32_t)kThreads : kLibLanes;
+}
 template <int W>
 LibFn lib_kernel_w(int la) {
 #ifdef LEOEC_MEASURE
-  if (la == 4) return &detail::lib_apply<W, 4>;
+  if (la == 4) return &detail::lib_apply<W, 4>;  // 256 lanes (lib_lanes())
   if (la == 8) return &detail::lib_apply<W, 8>;
+  if (lib_lanes() == (uint32_t)kThreads) return &detail::lib_apply<W, 2>;
 #endif
   (void)la;
-  return &detail::lib_apply<W, 2>;
+  return &detail::lib_apply<W, 2, kLibLanes>;
 }
 // Knobs::lib_xmap = 0 (A/B): workgroup ids in dispatch order instead of the
 // object-interleaved XCD map (xcd_obj_map, kernels_impl.hpp) that the
@@ -169,7 +181,9 @@ LibFn lib_kernel(int w) {
 
 int launch_lib(const BitApply& p, LibFn fn, hipStream_t s) {
   const uint32_t ps = (uint32_t)(p.block_size / (uint64_t)p.w);
-  const uint32_t tiles = (ps + kTileBytes - 1) / kTileBytes;
+  const uint32_t lanes = lib_lanes();
+  const uint32_t tb = lanes * 16u;
+  const uint32_t tiles = (ps + tb - 1) / tb;
   const uint64_t max_obj = (uint64_t)0x7FFFFFFF / tiles;
   for (uint64_t o0 = 0; o0 < p.nobj; o0 += max_obj) {
     const uint64_t no = (p.nobj - o0 < max_obj) ? p.nobj - o0 : max_obj;
@@ -188,7 +202,7 @@ int launch_lib(const BitApply& p, LibFn fn, hipStream_t s) {
       if (a.out[r].valid < vmin) vmin = a.out[r].valid;
     }
     a.vmin = vmin;
-    hipLaunchKernelGGL(fn, dim3((uint32_t)(no * tiles)), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL(fn, dim3((uint32_t)(no * tiles)), dim3(lanes), 0, s, a);
     if (hipGetLastError() != hipSuccess) return LEOEC_E_HIP;
   }
   return LEOEC_OK;

@@ -984,10 +984,13 @@ struct LibArgs {
 // wave per SIMD).
 constexpr int lib_waves(int w) { return w <= 7 ? 4 : w <= 11 ? 3 : 2; }
 
-template <int W, int LA>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(lib_waves(W), 8)))
+// TW: lanes per workgroup = 16-byte columns per tile (shipped 256: 4 KiB of
+// every packet; 64 = 1 KiB tiles, a measurement form).
+template <int W, int LA, int TW = kThreads>
+__global__ void __launch_bounds__(TW) __attribute__((amdgpu_waves_per_eu(lib_waves(W), 8)))
 lib_apply(const LibArgs a) {
   constexpr int RS = LA + 1;  // ring of packet registers: LA loads in flight
+  constexpr uint32_t kTileBytes = TW * 16u;
   const uint32_t bid = a.xmap ? xcd_obj_map(blockIdx.x, gridDim.x, a.tiles) : blockIdx.x;
   const uint32_t obj = bid / a.tiles;
   const uint32_t tile = bid - obj * a.tiles;

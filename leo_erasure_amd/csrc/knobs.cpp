@@ -54,6 +54,7 @@ const Knobs* read_env() {
   if (k->bit_form < 0 || k->bit_form > 9) k->bit_form = 4;
   k->lib_form = env_int("LEOEC_LIB_FORM", k->lib_form);
   k->lib_la = env_int("LEOEC_LIB_LA", k->lib_la);
+  k->lib_wg = env_int("LEOEC_LIB_WG", k->lib_wg);
   k->lib_xmap = env_int("LEOEC_LIB_XMAP", k->lib_xmap);
   k->gfbit_xmap = env_int("LEOEC_GFBIT_XMAP", k->gfbit_xmap);
   k->gfbit_lw = env_int("LEOEC_GFBIT_LW", k->gfbit_lw);

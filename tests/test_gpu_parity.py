@@ -304,13 +304,19 @@ def test_bitmatrix_kernel_forms_agree(gpu, le, oracle, form, measure):
         assert st == "ok" and rep == [blocks[0], blocks[k]]
 
 
-@pytest.mark.parametrize("form", ["0", "1"])
+@pytest.mark.parametrize("form", ["0", "1", "1-wg256", "1-la4"])
 def test_liberation_encode_forms(gpu, le, oracle, form, measure):
     """lib_apply (the liberation bitmatrix structure compiled in, LEOEC_LIB_FORM=1,
-    shipped) and the generic masked bitmatrix kernel (0): every instantiated w,
-    k from 1 to w, sizes with ragged tails, against the oracle; decode and
-    repair (generic kernel) of what was encoded."""
-    measure.setenv("LEOEC_LIB_FORM", form)
+    shipped with 64-lane, 1 KiB tiles; "1-wg256": the 256-lane, 4 KiB-tile
+    form; "1-la4": 4 packets of look-ahead, 256 lanes) and the generic masked
+    bitmatrix kernel (0): every instantiated w, k from 1 to w, sizes with
+    ragged tails, against the oracle; decode and repair (generic kernel) of
+    what was encoded."""
+    measure.setenv("LEOEC_LIB_FORM", form[0])
+    if form.endswith("wg256"):
+        measure.setenv("LEOEC_LIB_WG", "256")
+    if form.endswith("la4"):
+        measure.setenv("LEOEC_LIB_LA", "4")
     for w in (3, 5, 7, 11, 13):
         for k in sorted({1, 2, (w + 1) // 2, w}):
             for size in (1, 4097, 150001):
