@@ -286,13 +286,22 @@ int launch(const GfApply& p, hipStream_t s) {
 
 namespace {
 using LibDecFn = void (*)(const detail::LibDecArgs);
+// Knobs::lib_dec_wg = 64 (measurement build): 64-lane workgroups, 1 KiB tiles.
+uint32_t lib_dec_lanes() { return kMeasureBuild && knobs().lib_dec_wg == 64 ? 64u : (uint32_t)kThreads; }
+template <int W>
+LibDecFn lib_dec_kernel_w() {
+#ifdef LEOEC_MEASURE
+  if (lib_dec_lanes() == 64) return &detail::lib_dec_apply<W, 64>;
+#endif
+  return &detail::lib_dec_apply<W>;
+}
 LibDecFn lib_dec_kernel(int w) {
   switch (w) {
-    case 3: return &detail::lib_dec_apply<3>;
-    case 5: return &detail::lib_dec_apply<5>;
-    case 7: return &detail::lib_dec_apply<7>;
-    case 11: return &detail::lib_dec_apply<11>;
-    case 13: return &detail::lib_dec_apply<13>;
+    case 3: return lib_dec_kernel_w<3>();
+    case 5: return lib_dec_kernel_w<5>();
+    case 7: return lib_dec_kernel_w<7>();
+    case 11: return lib_dec_kernel_w<11>();
+    case 13: return lib_dec_kernel_w<13>();
     default: return nullptr;
   }
 }
@@ -315,7 +324,9 @@ int launch(const LibDecApply& p, hipStream_t s) {
     for (const Shard& sh : *v)
       if (sh.base && (((uintptr_t)sh.base & 15u) || (sh.stride & 15u))) return LEOEC_E_ARG;
   const uint32_t ps = (uint32_t)(p.block_size / (uint64_t)w);
-  const uint32_t tiles = (ps + kTileBytes - 1) / kTileBytes;
+  const uint32_t lanes = lib_dec_lanes();
+  const uint32_t tb = lanes * 16u;
+  const uint32_t tiles = (ps + tb - 1) / tb;
   const uint64_t max_obj = (uint64_t)0x7FFFFFFF / tiles;
   for (uint64_t o0 = 0; o0 < p.nobj; o0 += max_obj) {
     const uint64_t no = (p.nobj - o0 < max_obj) ? p.nobj - o0 : max_obj;
@@ -340,7 +351,7 @@ int launch(const LibDecApply& p, hipStream_t s) {
         a.mbits[b][q] = (b < nout && q < 2 * w) ? p.mbits[(size_t)b * 2 * w + q] : 0u;
     }
     a.vmin = vmin;
-    hipLaunchKernelGGL(fn, dim3((uint32_t)(no * tiles)), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL(fn, dim3((uint32_t)(no * tiles)), dim3(lanes), 0, s, a);
     if (hipGetLastError() != hipSuccess) return LEOEC_E_HIP;
   }
   return LEOEC_OK;

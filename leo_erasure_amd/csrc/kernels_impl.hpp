@@ -1074,9 +1074,11 @@ struct LibDecArgs {
 
 constexpr int lib_dec_waves(int w) { return w <= 5 ? 4 : w <= 11 ? 3 : 2; }
 
-template <int W>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(lib_dec_waves(W), 8)))
+// TW: lanes per workgroup = 16-byte columns per tile (as lib_apply).
+template <int W, int TW = kThreads>
+__global__ void __launch_bounds__(TW) __attribute__((amdgpu_waves_per_eu(lib_dec_waves(W), 8)))
 lib_dec_apply(const LibDecArgs a) {
+  constexpr uint32_t kTileBytes = TW * 16u;
   const uint32_t bid = a.xmap ? xcd_obj_map(blockIdx.x, gridDim.x, a.tiles) : blockIdx.x;
   const uint32_t obj = bid / a.tiles;
   const uint32_t tile = bid - obj * a.tiles;

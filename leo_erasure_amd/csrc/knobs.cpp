@@ -55,6 +55,7 @@ const Knobs* read_env() {
   k->lib_form = env_int("LEOEC_LIB_FORM", k->lib_form);
   k->lib_la = env_int("LEOEC_LIB_LA", k->lib_la);
   k->lib_wg = env_int("LEOEC_LIB_WG", k->lib_wg);
+  k->lib_dec_wg = env_int("LEOEC_LIB_DEC_WG", k->lib_dec_wg);
   k->lib_xmap = env_int("LEOEC_LIB_XMAP", k->lib_xmap);
   k->gfbit_xmap = env_int("LEOEC_GFBIT_XMAP", k->gfbit_xmap);
   k->gfbit_lw = env_int("LEOEC_GFBIT_LW", k->gfbit_lw);

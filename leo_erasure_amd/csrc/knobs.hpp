@@ -41,6 +41,7 @@ struct Knobs {
   int lib_form = 1;          // LEOEC_LIB_FORM=0: liberation through the generic bitmatrix kernel
   int lib_la = 2;            // LEOEC_LIB_LA: lib_apply packet look-ahead
   int lib_wg = 64;           // LEOEC_LIB_WG=256: lib_apply with 256-lane workgroups (4 KiB tiles)
+  int lib_dec_wg = 256;      // LEOEC_LIB_DEC_WG=64: lib_dec_apply with 64-lane workgroups
   int lib_xmap = 2;          // LEOEC_LIB_XMAP=0: liberation kernels without xcd_obj_map
   // gfbit_inst.hip
   int gfbit_xmap = -1;       // LEOEC_GFBIT_XMAP: 0 off, 1 object-contiguous, unset auto
