@@ -110,6 +110,7 @@ class GpuBackend:
         self.le = le
         self.device = torch.device("cuda", self.index)
         self.name = f"cuda:{self.index} {torch.cuda.get_device_name(self.index)}"
+        self.lib_path = le._lib.library_path()
 
     def random_batch(self, n, size, seed):
         t = self.torch
@@ -157,6 +158,59 @@ def cpu_share():
                      "threads_basis": basis}
 
 
+def _cpu_list(text):
+    """'0-3,8,10-11' -> [0, 1, 2, 3, 8, 10, 11]"""
+    out = []
+    for part in text.strip().split(","):
+        if part:
+            lo, _, hi = part.partition("-")
+            out.extend(range(int(lo), int(hi or lo) + 1))
+    return out
+
+
+def pick_cpus(threads, sysfs="/sys/devices/system"):
+    """CPUs to pin the baseline's `threads` workers to: one hardware thread
+    per physical core (no two workers on SMT siblings), from the NUMA node
+    this process runs on first, then the other nodes, within the affinity
+    mask (the cgroup's cpuset).  Returns (cpus, {numa nodes used})."""
+    aff = sorted(os.sched_getaffinity(0))
+    allowed = set(aff)
+
+    def read(path):
+        try:
+            with open(path) as fh:
+                return fh.read()
+        except OSError:
+            return None
+
+    node_of = {}
+    for nd in range(64):
+        t = read(f"{sysfs}/node/node{nd}/cpulist")
+        if t is None:
+            continue
+        for c in _cpu_list(t):
+            node_of[c] = nd
+    try:
+        import ctypes
+        here = ctypes.CDLL(None).sched_getcpu()
+    except (OSError, AttributeError):
+        here = aff[0]
+    home = node_of.get(here, 0)
+    seen_cores, first, rest = set(), [], []
+    for c in aff:
+        sib = read(f"{sysfs}/cpu/cpu{c}/topology/thread_siblings_list")
+        core = min(_cpu_list(sib)) if sib else c
+        if core in seen_cores:
+            continue
+        seen_cores.add(core)
+        (first if node_of.get(c, 0) == home else rest).append(c)
+    cpus = (first + rest)[:threads]
+    if len(cpus) < threads:  # fewer physical cores than threads: reuse siblings
+        cpus += [c for c in aff if c not in cpus][: threads - len(cpus)]
+    cpus = [c for c in cpus if c in allowed]
+    return cpus, sorted({node_of.get(c, 0) for c in cpus})
+
+
 def cpu_baseline(objs, parity, size, n_sample, target_s):
     """The CPU restatement with ISA-L's split-table / GFNI technique
     (oracle/leoec_oracle.c orc_bench_rs8), timed on this host's cores over a
@@ -169,30 +223,23 @@ def cpu_baseline(objs, parity, size, n_sample, target_s):
     from oracle import oracle as O
 
     threads, share = cpu_share()
+    cpus, nodes = pick_cpus(threads)
+    threads = len(cpus) or threads
     n = min(n_sample, objs.shape[0])
     host = objs[:n].to("cpu", copy=True).numpy()
     gpu_par = parity[:n].to("cpu", copy=True).numpy()
     cpu_par = np.zeros_like(gpu_par)
-    O.bench_rs8(0, K, M, host, size, size, n, cpu_par, threads=threads)
-    parity_ok = bool(np.array_equal(cpu_par, gpu_par))
-    # passes of >= target/12 s each (several encode+decode rounds), so that a
-    # pass is long against scheduler and memory-bandwidth noise from other
-    # tenants of the host; value = the median pass
+    # one pool of workers for the whole baseline, worker t pinned to cpus[t],
+    # each first-touching its own slice of the sample (NUMA-local pages);
+    # passes of >= target/12 s each (several encode+decode rounds between
+    # barriers); value = the median pass.  cpu_par receives the workers'
+    # encode of the sample, compared with the GPU's parity after the clock.
     pass_s = target_s / 12.0
-    rates = []
-    t_all = 0.0
-    while t_all < target_s or len(rates) < 3:
-        t0 = time.perf_counter()
-        reps = 0
-        while True:
-            O.bench_rs8(0, K, M, host, size, size, n, cpu_par, threads=threads)
-            O.bench_rs8(1, K, M, host, size, size, n, cpu_par, erased=ERASED, threads=threads)
-            reps += 1
-            dt = time.perf_counter() - t0
-            if dt >= pass_s:
-                break
-        t_all += dt
-        rates.append(2 * n * size * reps / dt / 2**30)
+    t0 = time.perf_counter()
+    rates = O.bench_rs8_pinned(K, M, host, size, ERASED, threads, cpus, pass_s, target_s,
+                               min_passes=3, parity_out=cpu_par)
+    t_all = time.perf_counter() - t0
+    parity_ok = bool(np.array_equal(cpu_par, gpu_par))
     rates.sort()
     med = rates[len(rates) // 2]
     rec = {
@@ -202,7 +249,9 @@ def cpu_baseline(objs, parity, size, n_sample, target_s):
         "sample": f"{len(rates)} passes of >= {pass_s:.2f} s over the first {n} x {size} B objects "
                   f"of rank 0's batch: "
                   f"vandrs RS({K},{M},8) encode + in-place decode of data blocks {ERASED}, "
-                  f"{threads} threads, {t_all:.2f} s; value = median pass",
+                  f"{threads} threads pinned one per physical core, each first-touching its "
+                  f"own slice, {t_all:.2f} s; value = median pass",
+        "pinning": {"cpus": cpus, "numa_nodes": nodes, "first_touch": "per worker thread"},
         "pass_spread": round((rates[-1] - rates[0]) / med, 4) if med else None,
         "iqr_spread": round((rates[(3 * len(rates)) // 4] - rates[len(rates) // 4]) / med, 4)
         if med else None,
@@ -213,6 +262,42 @@ def cpu_baseline(objs, parity, size, n_sample, target_s):
 
 
 # ---------------------------------------------------------------------------
+def read_traffic(paths, n, size, lib_path):
+    """PMC HBM bytes per encode launch from the committed measurement whose
+    batch shape matches (tools/pmc_traffic.py), or None.  The file carries
+    the sha256 of the code object it was measured on (the offload bundle
+    defining gf8_apply<10,4>, leo_erasure_amd/codeobj.py); the figure is
+    used only if the library this run loaded holds the same code object, so
+    a kernel change without a fresh PMC pass prints null, not a stale
+    number.  Returns (traffic, what was found)."""
+    from leo_erasure_amd import codeobj
+
+    have = None
+    for tpath in [t for t in paths.split(",") if t]:
+        if not os.path.exists(tpath):
+            continue
+        try:
+            with open(tpath) as fh:
+                tr = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if tr.get("objects") != n or tr.get("object_bytes") != size:
+            continue
+        want = (tr.get("code_object") or {}).get("sha256")
+        if have is None:
+            try:
+                have = codeobj.kernel_code_object_sha256(lib_path) if lib_path else ""
+            except (OSError, ValueError):
+                have = ""
+        name = os.path.basename(tpath)
+        if not want:
+            return None, f"{name}: no code-object stamp"
+        if want != have:
+            return None, f"{name}: stamp {want[:12]} != loaded code object {(have or '?')[:12]}"
+        return tr.get("encode_bytes_per_launch"), f"{name} (code object {want[:12]})"
+    return None, "no PMC file for this batch shape"
+
+
 def _poison_decode(be, objs, ref, parity, size, bs, erased):
     """Overwrite the erased data blocks, rebuild them, require the batch to
     equal its pristine copy: a decode that writes nothing fails this."""
@@ -313,17 +398,7 @@ def run_rank(args, be, rank, world, dist=None):
     dec_bytes = (K + len(ERASED)) * bs * n    # per decode launch
     enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
-    traffic = None
-    for tpath in [t for t in args.traffic.split(",") if t]:
-        if traffic is not None or not os.path.exists(tpath):
-            continue
-        try:
-            with open(tpath) as fh:
-                tr = json.load(fh)
-            if tr.get("objects") == n and tr.get("object_bytes") == size:
-                traffic = tr.get("encode_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    traffic, traffic_src = read_traffic(args.traffic, n, size, getattr(be, "lib_path", None))
     strong = global_n is not None
     rec = {
         "metric": METRIC_64 if strong else METRIC,
@@ -353,6 +428,7 @@ def run_rank(args, be, rank, world, dist=None):
             "bound": "hbm", "kernel": "gf8_apply<10,4> (encode)",
             "achieved": round(enc_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(enc_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": traffic_src,
             "alg_bytes_per_launch": enc_bytes, "avg_launch_ms": round(enc_ms, 4),
             "decode": {"achieved": round(dec_gbs, 1), "frac": round(dec_gbs / HBM_PEAK_GBS, 4),
                        "alg_bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_ms, 4)},

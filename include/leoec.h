@@ -146,8 +146,18 @@ int leoec_repair_dev(int coding, int k, int m, int w, const uint8_t *const *bloc
  * 0/1 bitmatrix as bytes (cauchyrs, liberation).  *n_out = entries written. */
 int leoec_coding_matrix(int coding, int k, int m, int w, uint32_t *out, int cap, int *n_out);
 
-/* Device ordinal in use, or a negative status. */
+/* Device ordinal the calling thread's device-resident calls (*_dev) use,
+ * or a negative status. */
 int leoec_device(void);
+
+/* Host-memory calls (leoec_encode / _decode / _repair) are spread over the
+ * node's gfx950 devices: each call goes to the dispatcher lane with the
+ * fewest calls in progress (one lane per device, each with its own batching
+ * queue and PCIe link); the caller's current device is left as it was.
+ * Returns the number of lanes and writes the device ordinal of lane i to
+ * devices[i] for i < cap (devices may be NULL), or a negative status.
+ * (No reference counterpart: the reference is CPU-only.) */
+int leoec_host_lanes(int *devices, int cap);
 
 /* Library version string. */
 const char *leoec_version(void);

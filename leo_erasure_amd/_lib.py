@@ -28,12 +28,13 @@ E_INVALID_CODING = -1
 E_NOT_ENOUGH_BLOCKS = -9
 E_NOT_UNIQUE = -10
 E_NO_DEVICE = -16
+E_HIP = -17
 
 # Every symbol declared in include/leoec.h (tests check the export table).
 EXPORTS = (
     "leoec_strerror", "leoec_gf_init", "leoec_check_params", "leoec_layout", "leoec_encode",
     "leoec_decode", "leoec_repair", "leoec_encode_dev", "leoec_decode_dev", "leoec_repair_dev",
-    "leoec_coding_matrix", "leoec_device", "leoec_version",
+    "leoec_coding_matrix", "leoec_device", "leoec_host_lanes", "leoec_version",
 )
 
 
@@ -63,6 +64,7 @@ def _load(path=LIB_PATH):
     L.leoec_version.restype = ctypes.c_char_p
     L.leoec_gf_init.argtypes = []
     L.leoec_device.argtypes = []
+    L.leoec_host_lanes.argtypes = [ctypes.POINTER(c_int), c_int]
     L.leoec_check_params.argtypes = [c_int] * 4
     L.leoec_layout.argtypes = [c_int] * 4 + [u64, ctypes.POINTER(u64), ctypes.POINTER(c_int)]
     L.leoec_encode.argtypes = [c_int] * 4 + [u8p, u64, u8p, u64]
@@ -135,3 +137,13 @@ def check(rc):
 
 def version():
     return lib.leoec_version().decode()
+
+
+def host_lanes():
+    """Device ordinal of each lane the host-memory calls are spread over."""
+    n = lib.leoec_host_lanes(None, 0)
+    if n < 0:
+        raise LeoecError(n)
+    arr = (ctypes.c_int * max(n, 1))()
+    check(min(0, lib.leoec_host_lanes(arr, n)))
+    return list(arr[:n])

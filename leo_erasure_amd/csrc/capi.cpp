@@ -6,6 +6,7 @@
 
 #include "../../include/leoec.h"
 #include "engine.hpp"
+#include "hostq.hpp"
 
 #define LEOEC_VERSION "0.1.0"
 
@@ -143,6 +144,17 @@ int leoec_device(void) {
     if (rc) return rc;
     int dev = 0;
     return hipGetDevice(&dev) == hipSuccess ? dev : (int)LEOEC_E_HIP;
+  });
+}
+
+int leoec_host_lanes(int* devices, int cap) {
+  return guarded([&] {
+    int rc = leoec::device_init();
+    if (rc) return rc;
+    const int n = leoec::hostq_lanes();
+    const std::vector<int>& d = leoec::host_devices();
+    for (int i = 0; devices && i < n && i < cap; ++i) devices[i] = d[(size_t)i % d.size()];
+    return n;
   });
 }
 

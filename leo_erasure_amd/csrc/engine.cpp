@@ -202,9 +202,8 @@ int bit_rows(const Code& c, const int* surv, const int* want, int nwant,
 // sends the caller to the generic bitmatrix path (wanted coding blocks,
 // encode).  E = data ids missing from S, C = coding ids in S, |C| = |E|;
 // the map is rows(wanted) of (B_CE)^-1 applied to S_C = B_CS' D_S' ^ C.
-int lib_dec_plan(const Code& c, const int* surv, const std::vector<Shard>& in, const int* want,
-                 const std::vector<Shard>& out, LibDecApply* p) {
-  const int k = c.k, w = c.w, nwant = (int)out.size();
+int lib_dec_plan(const Code& c, const int* surv, const int* want, int nwant, Plan* p) {
+  const int k = c.k, w = c.w;
   if (c.m != 2 || nwant < 1 || nwant > 2) return LEOEC_E_UNSUPPORTED;
   std::vector<int> pos(k + 2, -1);  // id -> index in `in`
   for (int i = 0; i < k; ++i) {
@@ -233,15 +232,7 @@ int lib_dec_plan(const Code& c, const int* surv, const std::vector<Shard>& in, c
           if (c.B.get(C[ic] * w + r, E[ie] * w + x)) A.set(ic * w + r, ie * w + x, true);
   const int rc = bit_invert(A, &inv);
   if (rc) return rc;
-  p->w = w;
-  p->k = k;
-  p->data.assign(k, Shard{nullptr, 0, 0});
-  for (int j = 0; j < k; ++j)
-    if (pos[j] >= 0) p->data[j] = in[pos[j]];
-  p->cod.assign(2, Shard{nullptr, 0, 0});
-  for (int r = 0; r < 2; ++r)
-    if (pos[k + r] >= 0) p->cod[r] = in[pos[k + r]];
-  p->out = out;
+  p->lib_pos = pos;
   p->mbits.assign((size_t)nwant * 2 * w, 0u);
   for (int b = 0; b < nwant; ++b)
     for (int x = 0; x < w; ++x)
@@ -252,77 +243,183 @@ int lib_dec_plan(const Code& c, const int* surv, const std::vector<Shard>& in, c
   return LEOEC_OK;
 }
 
-int apply(const Code& c, const int* surv, const std::vector<Shard>& in, const int* want,
-          const std::vector<Shard>& out, uint64_t bs, uint64_t nobj, hipStream_t s) {
-  const int nwant = (int)out.size();
-  if (nwant == 0 || nobj == 0 || bs == 0) return LEOEC_OK;
+namespace {
+
+int build_plan(const Code& c, const int* surv, const int* want, int nwant, Plan* p) {
+  p->code = &c;
+  p->surv.assign(surv, surv + c.k);
+  p->want.assign(want, want + nwant);
   if (!c.bitmatrix) {
-    GfApply p;
-    p.w = c.w;
-    p.K = c.k;
-    p.R = nwant;
-    int rc = gf_rows(c, surv, want, nwant, &p.coef);
-    if (rc) return rc;
-    p.in = in;
-    p.out = out;
-    p.block_size = bs;
-    p.nobj = nobj;
-    return launch(p, s);
+    p->kind = Plan::kGf;
+    return gf_rows(c, surv, want, nwant, &p->coef);
   }
   if (c.coding == LEOEC_CAUCHYRS && gfbit_supported(c.w) && knobs().bitmatrix == 0) {
     // cauchyrs bitmatrices (coding and decoding) are bit expansions of GF(2^w)
     // matrices: apply the GF map on the packet-bitsliced blocks directly
-    GfBitApply p;
-    p.w = c.w;
-    p.K = c.k;
-    p.R = nwant;
-    int rc = gf_rows(c, surv, want, nwant, &p.coef);
-    if (rc) return rc;
-    p.in = in;
-    p.out = out;
-    p.block_size = bs;
-    p.nobj = nobj;
-    return launch(p, s);
+    p->kind = Plan::kGfBit;
+    return gf_rows(c, surv, want, nwant, &p->coef);
   }
   if (c.coding == LEOEC_LIBERATION && lib_dec_supported(c.w)) {
-    LibDecApply p;
-    const int rc = lib_dec_plan(c, surv, in, want, out, &p);
-    if (rc == LEOEC_OK) {
-      p.block_size = bs;
-      p.nobj = nobj;
-      return launch(p, s);
-    }
+    p->kind = Plan::kLibDec;
+    const int rc = lib_dec_plan(c, surv, want, nwant, p);
     if (rc != LEOEC_E_UNSUPPORTED) return rc;  // else: the generic bitmatrix path
   }
-  BitApply p;
-  p.w = c.w;
-  p.KB = c.k;
-  p.RB = nwant;
-  int rc = bit_rows(c, surv, want, nwant, &p.bits);
+  p->kind = Plan::kBit;
+  return bit_rows(c, surv, want, nwant, &p->bits);
+}
+
+// Plans by (code, knobs that pick a kernel family, survivors, wanted ids).
+// Bounded: past kPlanCacheMax entries the cache starts over (plans in use
+// live on through their shared_ptr).
+constexpr size_t kPlanCacheMax = 4096;
+
+}  // namespace
+
+int make_plan(const Code& c, const int* surv, const int* want, int nwant,
+              std::shared_ptr<const Plan>* out) {
+  static std::mutex mu;
+  static std::map<std::vector<intptr_t>, std::shared_ptr<const Plan>> cache;
+  std::vector<intptr_t> key;
+  key.reserve(4 + c.k + nwant);
+  key.push_back((intptr_t)&c);
+  key.push_back(knobs().bitmatrix);
+  key.push_back(knobs().lib_form);
+  key.push_back(nwant);
+  key.insert(key.end(), surv, surv + c.k);
+  key.insert(key.end(), want, want + nwant);
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) {
+      *out = it->second;
+      return LEOEC_OK;
+    }
+  }
+  auto p = std::make_shared<Plan>();
+  const int rc = build_plan(c, surv, want, nwant, p.get());  // outside the lock
   if (rc) return rc;
-  p.in = in;
-  p.out = out;
-  p.block_size = bs;
-  p.nobj = nobj;
-  return launch(p, s);
+  std::lock_guard<std::mutex> lock(mu);
+  if (cache.size() >= kPlanCacheMax) cache.clear();
+  *out = cache.emplace(std::move(key), std::move(p)).first->second;
+  return LEOEC_OK;
+}
+
+int run_plan(const Plan& p, const std::vector<Shard>& in, const std::vector<Shard>& out,
+             uint64_t bs, uint64_t nobj, hipStream_t s) {
+  const Code& c = *p.code;
+  const int nwant = (int)out.size();
+  if (nwant == 0 || nobj == 0 || bs == 0) return LEOEC_OK;
+  if (nwant != (int)p.want.size() || (int)in.size() != c.k) return LEOEC_E_ARG;
+  switch (p.kind) {
+    case Plan::kGf: {
+      GfApply a;
+      a.w = c.w;
+      a.K = c.k;
+      a.R = nwant;
+      a.coef = p.coef;
+      a.in = in;
+      a.out = out;
+      a.block_size = bs;
+      a.nobj = nobj;
+      return launch(a, s);
+    }
+    case Plan::kGfBit: {
+      GfBitApply a;
+      a.w = c.w;
+      a.K = c.k;
+      a.R = nwant;
+      a.coef = p.coef;
+      a.in = in;
+      a.out = out;
+      a.block_size = bs;
+      a.nobj = nobj;
+      return launch(a, s);
+    }
+    case Plan::kLibDec: {
+      LibDecApply a;
+      a.w = c.w;
+      a.k = c.k;
+      a.data.assign(c.k, Shard{nullptr, 0, 0});
+      for (int j = 0; j < c.k; ++j)
+        if (p.lib_pos[j] >= 0) a.data[j] = in[p.lib_pos[j]];
+      a.cod.assign(2, Shard{nullptr, 0, 0});
+      for (int r = 0; r < 2; ++r)
+        if (p.lib_pos[c.k + r] >= 0) a.cod[r] = in[p.lib_pos[c.k + r]];
+      a.out = out;
+      a.mbits = p.mbits;
+      a.block_size = bs;
+      a.nobj = nobj;
+      return launch(a, s);
+    }
+    case Plan::kBit: {
+      BitApply a;
+      a.w = c.w;
+      a.KB = c.k;
+      a.RB = nwant;
+      a.bits = p.bits;
+      a.in = in;
+      a.out = out;
+      a.block_size = bs;
+      a.nobj = nobj;
+      return launch(a, s);
+    }
+  }
+  return LEOEC_E_ARG;
+}
+
+int apply(const Code& c, const int* surv, const std::vector<Shard>& in, const int* want,
+          const std::vector<Shard>& out, uint64_t bs, uint64_t nobj, hipStream_t s) {
+  const int nwant = (int)out.size();
+  if (nwant == 0 || nobj == 0 || bs == 0) return LEOEC_OK;
+  std::shared_ptr<const Plan> p;
+  const int rc = make_plan(c, surv, want, nwant, &p);
+  if (rc) return rc;
+  return run_plan(*p, in, out, bs, nobj, s);
 }
 
 // ---------------------------------------------------------------------------
 // Device and per-thread staging.
+namespace {
+std::vector<int> g_host_devices;  // written once, under device_init's call_once
+}  // namespace
+
 int device_init() {
   static std::once_flag once;
   static int status = LEOEC_E_NO_DEVICE;
   std::call_once(once, [] {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return;
-    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return;
-    status = LEOEC_OK;
+    for (int d = 0; d < n && d < kMaxDevices; ++d) {
+      hipDeviceProp_t prop;
+      if (hipGetDeviceProperties(&prop, d) != hipSuccess) continue;
+      if (std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) g_host_devices.push_back(d);
+    }
+    if (!g_host_devices.empty()) status = LEOEC_OK;
   });
   return status;
+}
+
+const std::vector<int>& host_devices() { return g_host_devices; }
+
+DeviceScope::DeviceScope(int dev) {
+  if (dev < 0) return;
+  if (hipGetDevice(&prev_) != hipSuccess) {
+    ok_ = false;
+    prev_ = -1;
+    return;
+  }
+  if (prev_ == dev) {
+    prev_ = -1;  // nothing to restore
+    return;
+  }
+  if (hipSetDevice(dev) != hipSuccess) {
+    ok_ = false;
+    prev_ = -1;
+  }
+}
+
+DeviceScope::~DeviceScope() {
+  if (prev_ >= 0) (void)hipSetDevice(prev_);
 }
 
 namespace {
@@ -392,7 +489,9 @@ struct Staging {
 // Record the loading thread at library load (static initialisation).
 const std::thread::id g_load_thread = Staging::load_thread();
 
-thread_local Staging tl_staging;  // one stream + device buffer per calling thread
+// one stream + device buffer per calling thread and device (host-memory
+// calls run on the device the dispatcher picks, hostq.cpp)
+thread_local Staging tl_staging[kMaxDevices];
 
 // Default (auto): gather when a direction has several separate host buffers
 // (decode / repair: k survivor binaries in, e rebuilt blocks out), pageable
@@ -593,14 +692,11 @@ int stage_d2h_sync(Staging* st, const std::vector<D2HSeg>& segs) {
 int get_staging(size_t bytes, Staging** out) {
   int rc = device_init();
   if (rc) return rc;
-  Staging& st = tl_staging;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return LEOEC_E_HIP;
+  if (dev < 0 || dev >= kMaxDevices) return LEOEC_E_NO_DEVICE;
+  Staging& st = tl_staging[dev];
   if (st.device != dev) {
-    if (st.device >= 0) {
-      st.release();  // buffers of the previous device (release() selects it)
-      if (hipSetDevice(dev) != hipSuccess) return LEOEC_E_HIP;
-    }
     if (hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking) != hipSuccess)
       return LEOEC_E_HIP;
     st.device = dev;
@@ -650,10 +746,12 @@ void pick_survivors(int coding, int k, const int* ids, const std::vector<int>& p
     if (present[id] >= 0) { surv->push_back(id); slot->push_back(present[id]); }
 }
 
-// Stage the k survivor blocks, run the map into nwant device outputs.
-int run_host_map(const Code& c, const uint8_t* const* blocks, const std::vector<int>& surv,
-                 const std::vector<int>& slot, const std::vector<int>& want, uint64_t bs,
-                 Staging** st_out, uint8_t** dev_out, uint64_t* stride_out) {
+// Stage the k survivor blocks, run the map into nwant device outputs (on the
+// calling thread's current device).
+int run_host_map(const Plan& plan, const uint8_t* const* blocks, const std::vector<int>& slot,
+                 uint64_t bs, Staging** st_out, uint8_t** dev_out, uint64_t* stride_out) {
+  const Code& c = *plan.code;
+  const std::vector<int>& want = plan.want;
   const int k = c.k;
   const uint64_t bs16 = round_to(bs, 16);
   if (c.bitmatrix && (bs % (16ull * (uint64_t)c.w))) return LEOEC_E_BAD_SIZE;
@@ -669,7 +767,7 @@ int run_host_map(const Code& c, const uint8_t* const* blocks, const std::vector<
   rc = stage_h2d_segs(st, st->buf, segs);
   uint8_t* outbase = st->buf + (uint64_t)k * bs16;
   for (size_t o = 0; o < want.size(); ++o) out[o] = Shard{outbase + o * bs16, 0, bs};
-  if (rc == LEOEC_OK) rc = apply(c, surv.data(), in, want.data(), out, bs16, 1, st->stream);
+  if (rc == LEOEC_OK) rc = run_plan(plan, in, out, bs16, 1, st->stream);
   if (rc) {
     // copies already queued may still read this thread's pinned buffer:
     // drain them before the next call reuses it
@@ -684,19 +782,16 @@ int run_host_map(const Code& c, const uint8_t* const* blocks, const std::vector<
 
 // The batched form of run_host_map's map (outputs left to the caller): the k
 // survivor blocks packed at bs16 spacing, outputs at bs16 spacing.
-void host_map_job(const Code& c, const uint8_t* const* blocks, const std::vector<int>& surv,
-                  const std::vector<int>& slot, const std::vector<int>& want, uint64_t bs,
-                  HostJob* J) {
+void host_map_job(const std::shared_ptr<const Plan>& plan, const uint8_t* const* blocks,
+                  const std::vector<int>& slot, uint64_t bs, HostJob* J) {
   const uint64_t bs16 = round_to(bs, 16);
-  const int k = c.k;
-  J->code = &c;
-  J->surv = surv;
-  J->want = want;
+  const int k = plan->code->k;
+  J->plan = plan;
   J->bs = J->in_blk = J->out_blk = bs16;
   J->in_valid.assign(k, bs);
   J->out_valid = bs;
   J->in_bytes = (uint64_t)k * bs16;
-  J->out_bytes = (uint64_t)want.size() * bs16;
+  J->out_bytes = (uint64_t)plan->want.size() * bs16;
   J->direct_cap = knobs().hostq_direct_map;
   for (int i = 0; i < k; ++i) J->in.push_back(HostSeg{blocks[slot[i]], (uint64_t)i * bs16, bs});
 }
@@ -744,12 +839,12 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
   std::vector<int> surv(k), want(m);
   for (int j = 0; j < k; ++j) surv[j] = j;
   for (int i = 0; i < m; ++i) want[i] = k + i;
+  std::shared_ptr<const Plan> plan;
+  if ((rc = make_plan(*c, surv.data(), want.data(), m, &plan))) return rc;
   HostqTicket ticket;
   {  // concurrent calls: one batched H2D / launch / D2H (hostq.cpp)
     HostJob J;
-    J.code = c;
-    J.surv = surv;
-    J.want = want;
+    J.plan = plan;
     J.bs = J.in_blk = J.out_blk = J.out_valid = bs;
     for (int j = 0; j < k; ++j) J.in_valid.push_back(clamp_valid(size, (uint64_t)j * bs, bs));
     J.in_bytes = round_to(size, 16);
@@ -760,6 +855,8 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
     rc = hostq_run(J, &ticket);
     if (rc != kNotBatched) return rc;
   }
+  DeviceScope on(ticket.device);  // the per-thread path, on the device the dispatcher picked
+  if (!on.ok()) return LEOEC_E_HIP;
   Staging* st;
   rc = get_staging((size_t)(k + m) * bs, &st);
   if (rc) return rc;
@@ -768,7 +865,7 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
     in[j] = Shard{st->buf + (uint64_t)j * bs, 0, clamp_valid(size, (uint64_t)j * bs, bs)};
   for (int i = 0; i < m; ++i) par[i] = Shard{st->buf + (uint64_t)(k + i) * bs, 0, bs};
   rc = stage_h2d_segs(st, st->buf, {H2DSeg{obj, 0, (size_t)size}});
-  if (rc == LEOEC_OK) rc = apply(*c, surv.data(), in, want.data(), par, bs, 1, st->stream);
+  if (rc == LEOEC_OK) rc = run_plan(*plan, in, par, bs, 1, st->stream);
   if (rc) {
     (void)hipStreamSynchronize(st->stream);  // queued copies may still read the caller's object
     return rc;
@@ -814,6 +911,7 @@ int op_decode(int coding, int k, int m, int w, const uint8_t* const* blocks, con
   uint8_t* dev = nullptr;
   uint64_t dstride = 0;
   HostqTicket ticket;
+  std::unique_ptr<DeviceScope> on;  // the per-thread path's device, up to the last copy
   if (!want.empty()) {
     const Code* c;
     rc = get_code(coding, k, m, w, &c);
@@ -822,14 +920,18 @@ int op_decode(int coding, int k, int m, int w, const uint8_t* const* blocks, con
     pick_survivors(coding, k, ids, present, &surv, &slot);
     const uint64_t bs16 = round_to(bs, 16);
     if (c->bitmatrix && (bs % (16ull * (uint64_t)w))) return LEOEC_E_BAD_SIZE;
+    std::shared_ptr<const Plan> plan;
+    if ((rc = make_plan(*c, surv.data(), want.data(), (int)want.size(), &plan))) return rc;
     HostJob J;
-    host_map_job(*c, blocks, surv, slot, want, bs, &J);
+    host_map_job(plan, blocks, slot, bs, &J);
     for (size_t o = 0; o < want.size(); ++o)
       J.out.push_back(OutSeg{out + (uint64_t)want[o] * bs, o * bs16,
                              clamp_valid(size, (uint64_t)want[o] * bs, bs)});
     rc = hostq_run(J, &ticket, &Survivors::copy, &survivors);
     if (rc != kNotBatched) return rc;
-    rc = run_host_map(*c, blocks, surv, slot, want, bs, &st, &dev, &dstride);
+    on.reset(new DeviceScope(ticket.device));
+    if (!on->ok()) return LEOEC_E_HIP;
+    rc = run_host_map(*plan, blocks, slot, bs, &st, &dev, &dstride);
     if (rc) return rc;
   }
   Survivors::copy(&survivors);
@@ -873,20 +975,24 @@ int op_repair(int coding, int k, int m, int w, const uint8_t* const* blocks, con
   std::vector<int> surv, slot;
   pick_survivors(coding, k, ids, present, &surv, &slot);
   if (c->bitmatrix && (bs % (16ull * (uint64_t)w))) return LEOEC_E_BAD_SIZE;
+  std::shared_ptr<const Plan> plan;
+  if ((rc = make_plan(*c, surv.data(), want.data(), (int)want.size(), &plan))) return rc;
   HostqTicket ticket;
   {
     const uint64_t bs16 = round_to(bs, 16);
     HostJob J;
-    host_map_job(*c, blocks, surv, slot, want, bs, &J);
+    host_map_job(plan, blocks, slot, bs, &J);
     for (size_t o = 0; o < want.size(); ++o)
       J.out.push_back(OutSeg{out + (uint64_t)pos[o] * bs, o * bs16, bs});
     rc = hostq_run(J, &ticket);
     if (rc != kNotBatched) return rc;
   }
+  DeviceScope on(ticket.device);
+  if (!on.ok()) return LEOEC_E_HIP;
   Staging* st;
   uint8_t* dev;
   uint64_t dstride;
-  rc = run_host_map(*c, blocks, surv, slot, want, bs, &st, &dev, &dstride);
+  rc = run_host_map(*plan, blocks, slot, bs, &st, &dev, &dstride);
   if (rc) return rc;
   std::vector<D2HSeg> segs;
   for (size_t o = 0; o < want.size(); ++o)

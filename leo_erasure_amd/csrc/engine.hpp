@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <vector>
 
 #include "codes.hpp"
@@ -29,12 +30,57 @@ int get_code(int coding, int k, int m, int w, const Code** out);  // cached
 int gf_rows(const Code& c, const int* surv, const int* want, int nwant, std::vector<uint32_t>* rows);
 int bit_rows(const Code& c, const int* surv, const int* want, int nwant, std::vector<uint8_t>* rows);
 
-// Enqueue "out blocks = map(survivor blocks)" for a batch.  in: k shards in
-// survivor order; out: nwant shards.
+// The map "out blocks = f(survivor blocks)" of one (code, survivors,
+// wanted ids), built on the host once: GF(2^w) coefficient rows (vandrs,
+// isars, cauchyrs through the packet-bitsliced kernel), GF(2) bit rows (the
+// generic bitmatrix kernel) or liberation's syndrome-decode masks.  All the
+// host arithmetic of a call (the k x k / kw x kw inversions) happens here, so
+// a plan that fails fails on the calling thread, before any device work.
+struct Plan {
+  enum Kind { kGf, kGfBit, kLibDec, kBit };
+  Kind kind = kGf;
+  const Code* code = nullptr;
+  std::vector<int> surv, want;
+  std::vector<uint32_t> coef;   // kGf, kGfBit: nwant x k
+  std::vector<uint8_t> bits;    // kBit: (nwant w) x (k w)
+  std::vector<int> lib_pos;     // kLibDec: id -> index of its shard in `in` (k + 2), -1 absent
+  std::vector<uint32_t> mbits;  // kLibDec: nwant x 2w
+};
+
+// Cached by (code, survivors, wanted ids): repeated erasure patterns reuse
+// their inverse.  The shared_ptr keeps a plan alive while a batch uses it.
+int make_plan(const Code& c, const int* surv, const int* want, int nwant,
+              std::shared_ptr<const Plan>* out);
+// Enqueue a plan over a batch.  in: k shards in survivor order; out: nwant.
+int run_plan(const Plan& p, const std::vector<Shard>& in, const std::vector<Shard>& out,
+             uint64_t block_size, uint64_t nobj, hipStream_t s);
+// make_plan + run_plan.
 int apply(const Code& c, const int* surv, const std::vector<Shard>& in, const int* want,
           const std::vector<Shard>& out, uint64_t block_size, uint64_t nobj, hipStream_t s);
 
-int device_init();  // opens the HIP device once; LEOEC_E_NO_DEVICE if unusable
+// Opens the HIP runtime once and lists its gfx950 devices; LEOEC_E_NO_DEVICE
+// if there is none.
+int device_init();
+// The gfx950 device ordinals the host-memory entry points spread their calls
+// over (valid after device_init() returned LEOEC_OK).
+const std::vector<int>& host_devices();
+constexpr int kMaxDevices = 64;
+
+// Makes `dev` the calling thread's current HIP device for a scope and puts
+// the previous one back (host-memory calls run on the device the dispatcher
+// picked without changing the caller's own device).
+class DeviceScope {
+ public:
+  explicit DeviceScope(int dev);
+  ~DeviceScope();
+  bool ok() const { return ok_; }
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+
+ private:
+  int prev_ = -1;
+  bool ok_ = true;
+};
 
 // Operations behind the C ABI (argument checking included).
 int op_layout(int coding, int k, int m, int w, uint64_t size, uint64_t* bs, int* filled);

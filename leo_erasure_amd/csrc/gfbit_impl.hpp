@@ -22,8 +22,7 @@ int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint6
   GfbArgs<R> a;
   a.K = nk;
   a.ps = (uint32_t)(p.block_size / (uint64_t)W);
-  constexpr uint32_t tb = WG * 4u * LW;
-  a.tiles = (a.ps + tb - 1) / tb;
+  a.tiles = packet_tiles(a.ps, WG, 4u * LW);
   for (int j = 0; j < kMaxK; ++j)
     a.in[j] = j < nk ? dev_shard(p.in[j0 + j], o0) : DevShard{nullptr, 0, 0, 0};
   for (int i = 0; i < R; ++i) {

@@ -192,10 +192,11 @@ GfbFn pick_measure8(int r, bool acc) {
   if (kn.gfbit_waves == 4) return pick_r_waves<8, 2, kPF, 4>(r, acc);
   if (kn.gfbit_waves == 5) return pick_r_waves<8, 2, kPF, 5>(r, acc);
   if (kn.gfbit_wg == 64) return pick_r_wg64<8, 2>(r, acc);
-  // LEOEC_GFBIT_WG=128: 16-byte lanes, next block's loads in flight.  (The
-  // load-then-compute form of this lane width faulted on the GPU in its first
-  // parity run, profiles/r02_v15_cauchy_lw16_pf0_abort.log, and is not built.)
-  if (kn.gfbit_wg == 128) return pick_r_wg<8, 4, 1, 128>(r, acc);
+  // LEOEC_GFBIT_WG=128: 16-byte lanes, next block's loads in flight
+  // (LEOEC_GFBIT_PF=0: load-then-compute; the round-2 abort of this form,
+  // profiles/r02_v15_cauchy_lw16_pf0_abort.log, is diagnosed in DESIGN.md)
+  if (kn.gfbit_wg == 128)
+    return kn.gfbit_pf == 0 ? pick_r_wg<8, 4, 0, 128>(r, acc) : pick_r_wg<8, 4, 1, 128>(r, acc);
   const int lw = kn.gfbit_lw;
   if (kn.gfbit_ceil && r == 4 && !acc) return &launch_gfb_t<8, 4, 2, false, kPF, true>;
   if (kn.gfbit_xmap == 1 && r == 4 && !acc)
@@ -303,7 +304,9 @@ int launch(const GfBitApply& p, hipStream_t s) {
   for (const Shard& sh : p.out)
     if (((uintptr_t)sh.base & 15u) || (sh.stride & 15u)) return LEOEC_E_ARG;
   const uint64_t ps = p.block_size / (uint64_t)w;
-  const uint64_t tiles = (ps + 1023) / 1024;  // smallest lane width -> most tiles
+  // the narrowest tile of any form (64 lanes x 8 bytes, LEOEC_GFBIT_WG=64)
+  // bounds the grid: every form's tile count is at most this
+  const uint64_t tiles = (ps + 511) / 512;
   const uint64_t max_obj = (uint64_t)0x7FFFFFFF / tiles;
   for (uint64_t o0 = 0; o0 < p.nobj; o0 += max_obj) {
     const uint64_t no = (p.nobj - o0 < max_obj) ? p.nobj - o0 : max_obj;

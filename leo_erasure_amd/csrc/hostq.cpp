@@ -12,6 +12,7 @@
 // in launch order and wakes their callers.
 #include "hostq.hpp"
 
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -51,8 +52,14 @@ void stat_add(int i, double x) {
   std::lock_guard<std::mutex> l(g_stats.mu);
   g_stats.v[i] += x;
 }
+double g_lane_jobs[64] = {};  // jobs launched per lane (under g_stats.mu)
+void stat_lane_jobs(int lane, double n) {
+  std::lock_guard<std::mutex> l(g_stats.mu);
+  if (lane >= 0 && lane < 64) g_lane_jobs[lane] += n;
+}
 #else
 inline void stat_add(int, double) {}
+inline void stat_lane_jobs(int, double) {}
 #endif
 
 enum class St { kFree, kOpen, kClosed, kInflight, kDone };
@@ -70,8 +77,10 @@ struct Slot {
   uint64_t used_in = 0, used_out = 0;
   std::vector<const HostJob*> jobs;
   std::vector<uint64_t> in_off, out_off;
+  std::vector<int> job_rc;  // per job: its launch's status
+  int lane = -1;
   int reserved = 0, filled = 0, readers = 0;
-  int status = LEOEC_OK;
+  int status = LEOEC_OK;    // the batch's copies and event: fails every job
   Clock::time_point opened, done;
 };
 
@@ -125,16 +134,22 @@ int slot_alloc(Slot* s) {
 }
 
 bool same_map(const HostJob& a, const HostJob& b) {
-  return a.code == b.code && a.bs == b.bs && a.in_blk == b.in_blk && a.out_blk == b.out_blk &&
+  return (a.plan == b.plan ||
+          (a.plan->code == b.plan->code && a.plan->surv == b.plan->surv &&
+           a.plan->want == b.plan->want && a.plan->kind == b.plan->kind)) &&
+         a.bs == b.bs && a.in_blk == b.in_blk && a.out_blk == b.out_blk &&
          a.out_valid == b.out_valid && a.in_bytes == b.in_bytes && a.out_bytes == b.out_bytes &&
-         a.surv == b.surv && a.want == b.want && a.in_valid == b.in_valid;
+         a.in_valid == b.in_valid;
 }
 
 // Enqueue one batch: ONE H2D of the input arena, one launch per run of
 // consecutive identical maps (their regions are uniformly strided: they were
 // reserved back to back with the same sizes), ONE D2H of the output arena.
-// The event is recorded whatever happened, so the completer always waits
-// for the work that was enqueued before the slot can be reused.
+// Plans were built by the callers, so a launch can fail only for its own
+// jobs (s->job_rc); the other runs are still launched.  The event is
+// recorded whatever happened, so the completer always waits for the work
+// that was enqueued before the slot can be reused.  Returns the status that
+// fails every job (the copies, the event).
 int launch_slot(Slot* s) {
   Clock::time_point t = Clock::now();
   int rc = hipMemcpyAsync(s->d_in, s->h_in, s->used_in, hipMemcpyHostToDevice, s->stream) ==
@@ -152,13 +167,22 @@ int launch_slot(Slot* s) {
     while (j < n && same_map(J, *s->jobs[j]) && s->in_off[j] == s->in_off[j - 1] + sin &&
            s->out_off[j] == s->out_off[j - 1] + sout)
       ++j;
-    const int k = (int)J.surv.size(), r = (int)J.want.size();
+    const int k = J.plan->code->k, r = (int)J.plan->want.size();
     std::vector<Shard> in(k), out(r);
     for (int b = 0; b < k; ++b)
       in[b] = Shard{s->d_in + s->in_off[i] + (uint64_t)b * J.in_blk, sin, J.in_valid[b]};
     for (int o = 0; o < r; ++o)
       out[o] = Shard{s->d_out + s->out_off[i] + (uint64_t)o * J.out_blk, sout, J.out_valid};
-    rc = apply(*J.code, J.surv.data(), in, J.want.data(), out, J.bs, (uint64_t)(j - i), s->stream);
+    int run_rc;
+#ifdef LEOEC_MEASURE
+    // fault injection (LEOEC_HOSTQ_FAIL_BS): this run's launch "fails"
+    if (knobs().hostq_fail_bs > 0 && J.bs == (uint64_t)knobs().hostq_fail_bs)
+      run_rc = LEOEC_E_HIP;
+    else
+#endif
+      run_rc = run_plan(*J.plan, in, out, J.bs, (uint64_t)(j - i), s->stream);
+    stat_lane_jobs(s->lane, (double)(j - i));
+    for (size_t x = i; x < j; ++x) s->job_rc[x] = run_rc;
     stat_add(2, 1);
     i = j;
   }
@@ -259,65 +283,109 @@ void completer_main(Queue* q) {
   }
 }
 
-// One queue per device, created on first use; its two threads live for the
-// process (they hold no GPU work when idle, and a process exits with them
-// parked on their condition variables).
-constexpr int kMaxDevices = 64;
+// Dispatcher lanes: lane i runs on host_devices()[i % ndev].  The product
+// has one lane per gfx950 device; the measurement knob LEOEC_HOSTQ_LANES
+// maps more lanes onto fewer devices (the dispatcher's test on a one-GPU
+// box).  Each lane has a queue, created on first use; its two threads live
+// for the process (they hold no GPU work when idle, and a process exits with
+// them parked on their condition variables; libleoec.so is linked
+// -z nodelete so their code is never unmapped).
+constexpr int kMaxLanes = 64;
 
-Queue* queue_for(int dev) {
+std::atomic<int> g_load[kMaxLanes];  // calls in progress per lane
+std::atomic<unsigned> g_rr{0};
+
+int lane_count() {
+  const int ndev = (int)host_devices().size();
+  const int want = knobs().hostq_lanes > 0 ? knobs().hostq_lanes : ndev;
+  return want < 1 ? 1 : (want > kMaxLanes ? kMaxLanes : want);
+}
+
+int lane_device(int lane) {
+  const std::vector<int>& d = host_devices();
+  return d[(size_t)lane % d.size()];
+}
+
+// The lane with the fewest calls in progress, ties broken round-robin.
+int pick_lane() {
+  const int n = lane_count();
+  const unsigned start = g_rr.fetch_add(1, std::memory_order_relaxed);
+  int best = (int)(start % (unsigned)n);
+  int best_load = g_load[best].load(std::memory_order_relaxed);
+  for (int i = 1; i < n && best_load > 0; ++i) {
+    const int l = (int)((start + (unsigned)i) % (unsigned)n);
+    const int x = g_load[l].load(std::memory_order_relaxed);
+    if (x < best_load) {
+      best = l;
+      best_load = x;
+    }
+  }
+  return best;
+}
+
+Queue* queue_for(int lane) {
   static std::mutex mu;
-  static Queue* queues[kMaxDevices] = {};
-  static bool failed[kMaxDevices] = {};
-  if (dev < 0 || dev >= kMaxDevices) return nullptr;
+  static Queue* queues[kMaxLanes] = {};
+  static bool failed[kMaxLanes] = {};
+  if (lane < 0 || lane >= kMaxLanes) return nullptr;
   std::lock_guard<std::mutex> lock(mu);
-  if (!queues[dev] && !failed[dev]) {
+  if (!queues[lane] && !failed[lane]) {
     // every slot's buffers up front, each touched once by a copy each way:
     // the first transfer through a new pinned buffer costs milliseconds,
     // which a caller should not pay inside the queue's lock
+    const int dev = lane_device(lane);
+    DeviceScope on(dev);
     Queue* q = new Queue;
     q->device = dev;
     for (Slot& sl : q->slots) {
-      if (slot_alloc(&sl) != LEOEC_OK ||
+      sl.lane = lane;
+      if (!on.ok() || slot_alloc(&sl) != LEOEC_OK ||
           hipMemcpyAsync(sl.d_in, sl.h_in, kSlotBytes, hipMemcpyHostToDevice, sl.stream) !=
               hipSuccess ||
           hipMemcpyAsync(sl.h_out, sl.d_out, kSlotBytes, hipMemcpyDeviceToHost, sl.stream) !=
               hipSuccess ||
           hipStreamSynchronize(sl.stream) != hipSuccess) {
-        failed[dev] = true;  // no batching on this device (pinned memory short): per-thread path
-        return nullptr;      // (the partial queue is leaked, as queues are)
+        failed[lane] = true;  // no batching on this lane (pinned memory short): per-thread path
+        return nullptr;       // (the partial queue is leaked, as queues are)
       }
     }
     std::thread(worker_main, q).detach();
     std::thread(completer_main, q).detach();
-    queues[dev] = q;
+    queues[lane] = q;
   }
-  return queues[dev];
+  return queues[lane];
 }
 
 }  // namespace
 
 HostqTicket::~HostqTicket() {
-  if (!queue) return;
-  Queue* q = static_cast<Queue*>(queue);
-  std::lock_guard<std::mutex> lock(q->mu);
-  --q->direct;
+  if (queue) {
+    Queue* q = static_cast<Queue*>(queue);
+    std::lock_guard<std::mutex> lock(q->mu);
+    --q->direct;
+  }
+  if (lane >= 0) g_load[lane].fetch_sub(1, std::memory_order_relaxed);
 }
 
+int hostq_lanes() { return device_init() == LEOEC_OK ? lane_count() : 0; }
+
 int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), void* arg) {
+  int rc = device_init();
+  if (rc) return rc;
+  const int lane = pick_lane();
+  g_load[lane].fetch_add(1, std::memory_order_relaxed);
+  ticket->lane = lane;  // charged until the call returns (~HostqTicket)
+  ticket->device = lane_device(lane);
   if (!knobs().host_batch) return kNotBatched;
   const uint64_t a_in = align_up(job.in_bytes), a_out = align_up(job.out_bytes);
   if (a_in == 0 || a_out == 0 || a_in > kBatchMaxJobBytes || a_out > kBatchMaxJobBytes)
     return kNotBatched;
-  int rc = device_init();
-  if (rc) return rc;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return LEOEC_E_HIP;
-  Queue* q = queue_for(dev);
+  Queue* q = queue_for(lane);
   if (!q) return kNotBatched;
 
   const Clock::time_point t0 = Clock::now();
   std::unique_lock<std::mutex> lk(q->mu);
-  if (ticket && q->direct < job.direct_cap && (!q->open || q->open->reserved == 0) &&
+  if (q->direct < job.direct_cap && (!q->open || q->open->reserved == 0) &&
       q->closed.empty() && q->inflight.empty()) {
     ++q->direct;  // idle queue, few callers: the per-thread path
     ticket->queue = q;
@@ -350,6 +418,7 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
     f->jobs.clear();
     f->in_off.clear();
     f->out_off.clear();
+    f->job_rc.clear();
     f->reserved = f->filled = f->readers = 0;
     f->status = LEOEC_OK;
     f->opened = std::chrono::steady_clock::now();
@@ -357,9 +426,11 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
   }
   stat_add(9, us_since(t0));
   const uint64_t oi = s->used_in, oo = s->used_out;
+  const size_t idx = s->jobs.size();
   s->used_in += a_in;
   s->used_out += a_out;
   s->jobs.push_back(&job);
+  s->job_rc.push_back(LEOEC_OK);
   s->in_off.push_back(oi);
   s->out_off.push_back(oo);
   ++s->reserved;
@@ -380,7 +451,7 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
   const Clock::time_point tw = Clock::now();
   q->cv_done.wait(lk, [s] { return s->state == St::kDone; });
   stat_add(8, us_since(tw));
-  const int status = s->status;
+  const int status = s->status != LEOEC_OK ? s->status : s->job_rc[idx];
   lk.unlock();
   if (status == LEOEC_OK)
     for (const OutSeg& g : job.out) std::memcpy(g.dst, s->h_out + oo + g.off, g.n);
@@ -406,6 +477,16 @@ extern "C" __attribute__((visibility("default"))) void leoec_measure_hostq_stats
   for (int i = 0; i < 14; ++i) {
     out14[i] = leoec::g_stats.v[i];
     leoec::g_stats.v[i] = 0;
+  }
+}
+
+// Measurement build: jobs launched per dispatcher lane since the last call
+// (batched jobs only); resets them.
+extern "C" __attribute__((visibility("default"))) void leoec_measure_hostq_lane_jobs(double* out64) {
+  std::lock_guard<std::mutex> l(leoec::g_stats.mu);
+  for (int i = 0; i < 64; ++i) {
+    out64[i] = leoec::g_lane_jobs[i];
+    leoec::g_lane_jobs[i] = 0;
   }
 }
 #endif

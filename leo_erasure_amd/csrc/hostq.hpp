@@ -15,6 +15,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <vector>
 
 #include "engine.hpp"
@@ -35,8 +36,7 @@ struct OutSeg {  // job output region -> caller buffer
 // (in_valid[i] bytes of it are real, the rest read as zero), output block o
 // at out_blk * o inside its output region.
 struct HostJob {
-  const Code* code = nullptr;
-  std::vector<int> surv, want;
+  std::shared_ptr<const Plan> plan;  // built on the caller's thread (engine.hpp make_plan)
   uint64_t bs = 0;  // kernel block geometry (multiple of 16)
   uint64_t in_blk = 0, out_blk = 0;
   std::vector<uint64_t> in_valid;  // per input block
@@ -51,25 +51,36 @@ struct HostJob {
 // per-thread path (their copies amortise their own submit cost).
 constexpr uint64_t kBatchMaxJobBytes = (uint64_t)8 << 20;
 
-// Held by a call that hostq_run sent to its per-thread path while the queue
-// was idle (few concurrent callers: their own streams and direct copies are
-// faster than a batch); released when the call returns.
+// Held by a call that hostq_run sent to its per-thread path: `device` is the
+// device it runs on (the dispatcher's pick; -1: the caller's current
+// device), and the call counts against that device's load until it returns.
 struct HostqTicket {
-  void* queue = nullptr;
+  int device = -1;
+  int lane = -1;         // dispatcher lane (logical queue) charged with the call
+  void* queue = nullptr; // set when the call holds one of the queue's direct places
   HostqTicket() = default;
   HostqTicket(const HostqTicket&) = delete;
   HostqTicket& operator=(const HostqTicket&) = delete;
   ~HostqTicket();
 };
 
-// Run `job` through the current device's queue and wait for it.  `overlap`
-// (may be null) runs on the caller's thread while the batch is on the GPU.
-// Returns a leoec_status, or kNotBatched: nothing was done and the caller
-// runs its per-thread path — the job is too large, batching is off, pinned
-// memory is short, or the queue is idle and fewer than job.direct_cap
-// calls are already running direct (`ticket` then counts this one).
+// Run `job` on one of the node's gfx950 devices and wait for it.  The
+// dispatcher gives each call the lane (one queue per device; the
+// measurement build can map more lanes onto fewer devices) with the fewest
+// calls in progress, ties taken round-robin, so concurrent callers spread
+// over every device and its PCIe link.  `overlap` (may be null) runs on the
+// caller's thread while the batch is on the GPU.  Returns a leoec_status
+// (this job's own: another caller's failed launch does not fail it), or
+// kNotBatched: nothing was done and the caller runs its per-thread path on
+// ticket->device — the job is too large, batching is off, pinned memory is
+// short, or the lane's queue is idle and fewer than job.direct_cap calls are
+// already running direct.
 constexpr int kNotBatched = 1;
 int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*) = nullptr,
               void* arg = nullptr);
+
+// Dispatcher lanes in use (one per gfx950 device in the product build), or
+// 0 without a device.
+int hostq_lanes();
 
 }  // namespace leoec

@@ -984,8 +984,10 @@ struct LibArgs {
 // wave per SIMD).
 constexpr int lib_waves(int w) { return w <= 7 ? 4 : w <= 11 ? 3 : 2; }
 
-// TW: lanes per workgroup = 16-byte columns per tile (shipped 256: 4 KiB of
-// every packet; 64 = 1 KiB tiles, a measurement form).
+// TW: lanes per workgroup = 16-byte columns per tile.  lib_apply ships with
+// 64 lanes (1 KiB of every packet per tile, kernels.hip kLibLanes); 256
+// lanes (4 KiB tiles) and the other look-ahead depths are measurement-build
+// forms.  (lib_dec_apply still ships with 256 lanes.)
 template <int W, int LA, int TW = kThreads>
 __global__ void __launch_bounds__(TW) __attribute__((amdgpu_waves_per_eu(lib_waves(W), 8)))
 lib_apply(const LibArgs a) {
@@ -1262,10 +1264,7 @@ template <int W, int LW>
 __device__ __forceinline__ void gfb_load_block(const uint8_t* base, uint32_t ps, uint32_t off,
                                                uint32_t bv, LaneVec<LW> (&y)[W]) {
 #pragma unroll
-  for (int x = 0; x < W; ++x) {
-    const uint32_t pk = (uint32_t)x * ps;
-    y[x] = lv_load<LW>(base + pk, off, bv > pk ? bv - pk : 0u);
-  }
+  for (int x = 0; x < W; ++x) y[x] = lv_load<LW>(base + (uint32_t)x * ps, off, packet_valid(bv, x, ps));
 }
 
 // acc[i] ^= c[i] * y for every output i (y is consumed: it is doubled in
@@ -1325,7 +1324,7 @@ gfbit_apply(const GfbArgs<R> a) {
                                                : blockIdx.x;
   const uint32_t obj = bid / a.tiles;
   const uint32_t tile = bid - obj * a.tiles;
-  const uint32_t off = tile * (WG * LB) + threadIdx.x * LB;
+  const uint32_t off = packet_lane_off(tile, threadIdx.x, WG, LB);
   if (off >= a.ps) return;
   const uint64_t o64 = obj;
   LaneVec<LW> acc[R][W];
@@ -1335,9 +1334,8 @@ gfbit_apply(const GfbArgs<R> a) {
     for (int x = 0; x < W; ++x) {
       if (ACC) {
         const uint32_t pk = (uint32_t)x * a.ps;
-        const uint32_t bv = a.out[i].valid;
         acc[i][x] = lv_load<LW>(a.out[i].base + o64 * a.out[i].stride + pk, off,
-                                bv > pk ? bv - pk : 0u);
+                                packet_valid(a.out[i].valid, x, a.ps));
       } else {
 #pragma unroll
         for (int e = 0; e < LW; ++e) acc[i][x].v[e] = 0u;
@@ -1385,11 +1383,10 @@ gfbit_apply(const GfbArgs<R> a) {
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     uint8_t* p = const_cast<uint8_t*>(a.out[i].base) + o64 * a.out[i].stride;
-    const uint32_t bv = a.out[i].valid;
 #pragma unroll
     for (int x = 0; x < W; ++x) {
       const uint32_t pk = (uint32_t)x * a.ps;
-      lv_store<LW>(p + pk, off, bv > pk ? bv - pk : 0u, acc[i][x]);
+      lv_store<LW>(p + pk, off, packet_valid(a.out[i].valid, x, a.ps), acc[i][x]);
     }
   }
 }

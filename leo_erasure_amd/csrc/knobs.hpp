@@ -27,6 +27,10 @@ struct Knobs {
                              //   path while the queue is idle (0: every call batched)
   int hostq_direct_map = 2;  // LEOEC_HOSTQ_DIRECT_MAP: the same for decode / repair (their
                              //   per-thread path gathers k buffers: it tops out sooner)
+  int hostq_fail_bs = 0;     // LEOEC_HOSTQ_FAIL_BS: batched launches of this block size report
+                             //   a HIP error (fault injection: per-job status)
+  int hostq_lanes = 0;       // LEOEC_HOSTQ_LANES: dispatcher lanes (0: one per gfx950 device;
+                             //   N: N lanes, lane i on device i % devices)
   // kernels.hip / kernels_impl.hpp
   int gf8_variant = 0;       // LEOEC_GF8_VARIANT: gf8_apply<10,4> variant (gf8_exp.hip)
   int gf8_tmap = 0;          // LEOEC_GF8_TMAP: gf8_apply workgroup -> tile order

@@ -42,5 +42,25 @@ LEOEC_TM_HD uint32_t xcd_obj_map(uint32_t b, uint32_t n, uint32_t tiles) {
   return ((i / tiles) * kXcds + x) * tiles + i % tiles;
 }
 
+// Lane geometry of the packet kernels (gfbit_apply, gfb2_apply): block bytes
+// bs = w packets of ps = bs / w bytes; a WG-lane workgroup (tile) covers
+// WG * LB bytes at the same offset of every packet of one object, lane l the
+// LB bytes at packet offset tile * WG * LB + l * LB.  Lanes at or past ps do
+// nothing.  tests/tile_maps_test.cpp checks, for every launch shape, that the
+// lanes write each valid output byte once and never read or write past a
+// block's valid length rounded up to the lane's chunk.
+LEOEC_TM_HD uint32_t packet_tiles(uint32_t ps, uint32_t wg, uint32_t lb) {
+  return (ps + wg * lb - 1u) / (wg * lb);
+}
+LEOEC_TM_HD uint32_t packet_lane_off(uint32_t tile, uint32_t lane, uint32_t wg, uint32_t lb) {
+  return tile * (wg * lb) + lane * lb;
+}
+// Data bytes of packet x in a block whose first `valid` bytes are data (the
+// rest of the block reads as zero and is never stored).
+LEOEC_TM_HD uint32_t packet_valid(uint32_t valid, uint32_t x, uint32_t ps) {
+  const uint32_t pk = x * ps;
+  return valid > pk ? valid - pk : 0u;
+}
+
 }  // namespace detail
 }  // namespace leoec

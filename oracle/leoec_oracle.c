@@ -14,6 +14,8 @@
 #include "leoec_oracle.h"
 
 #include <pthread.h>
+#include <sched.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 #if defined(__x86_64__)
@@ -817,13 +819,13 @@ typedef struct {
   const int *surv;      /* decode: survivor ids */
 } bench_job;
 
-static void *bench_worker(void *arg) {
-  bench_job *J = arg;
+/* One object of a bench job: RSCoding::doEncode's stripe staging, then the
+ * encode, or the in-place decode of the job's erased data blocks.  `tail` is
+ * a k*bs scratch buffer. */
+static void bench_object(const bench_job *J, int o, uint8_t *tail) {
   uint64_t bs = J->bs;
   int k = J->k, m = J->m;
-  uint8_t *tail = aligned_alloc(64, orc_round_to(bs * (uint64_t)k + 64, 64));
-  uint8_t *dec = aligned_alloc(64, orc_round_to(bs * (uint64_t)k + 64, 64));
-  for (int o = J->o0; o < J->o1; o++) {
+  {
     const uint8_t *obj = J->objs + (uint64_t)o * J->stride;
     uint8_t *par = J->parity + (uint64_t)o * m * bs;
     /* stripe staging exactly as RSCoding::doEncode: whole blocks alias the
@@ -866,20 +868,30 @@ static void *bench_worker(void *arg) {
         }
       }
   }
+}
+
+static void *bench_worker(void *arg) {
+  bench_job *J = arg;
+  uint8_t *tail = aligned_alloc(64, orc_round_to(J->bs * (uint64_t)J->k + 64, 64));
+  for (int o = J->o0; o < J->o1; o++) bench_object(J, o, tail);
   free(tail);
-  free(dec);
   return NULL;
 }
 
-int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride, uint64_t size,
-                  int nobj, uint8_t *parity, const int *erased, int nerased, int threads,
-                  int force_scalar) {
-  if (k <= 0 || m <= 0 || k + m > 256 || threads <= 0 || nerased > m) return ORC_E_PARAMS;
-  uint64_t bs = orc_block_size(k, 8, size);
+/* The coefficient tables of one bench op: encode, or the decode of the
+ * erased data blocks from the first k intact ids. */
+typedef struct {
+  int nout, surv[256], want[256];
+  uint8_t *tbl;   /* (m+k) x k x 32 split tables */
+  uint64_t *mats; /* nout x k GFNI matrices */
+} bench_plan;
+
+static int bench_plan_make(bench_plan *P, int op, int k, int m, const int *erased, int nerased) {
   uint32_t *C = malloc(sizeof(uint32_t) * m * k);
   uint32_t *rows = malloc(sizeof(uint32_t) * (m + k) * k);
-  uint8_t *tbl = malloc((size_t)(m + k) * k * 32);
-  int surv[256], want[256], nout;
+  P->tbl = malloc((size_t)(m + k) * k * 32);
+  P->mats = NULL;
+  int *surv = P->surv, *want = P->want, nout = 0;
   int rc = orc_vandermonde_coding_matrix(k, m, 8, C);
   if (rc) goto done;
   if (op == 0) {
@@ -901,9 +913,34 @@ int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride
     rc = decode_map_gf(ORC_VANDRS, k, m, 8, C, surv, want, nout, rows);
     if (rc) goto done;
   }
-  init_tables(nout, k, rows, tbl);
-  uint64_t *mats = malloc(sizeof(uint64_t) * (size_t)nout * k);
-  for (int i = 0; i < nout * k; i++) mats[i] = gfni_matrix(rows[i]);
+  P->nout = nout;
+  init_tables(nout, k, rows, P->tbl);
+  P->mats = malloc(sizeof(uint64_t) * (size_t)(nout ? nout : 1) * k);
+  for (int i = 0; i < nout * k; i++) P->mats[i] = gfni_matrix(rows[i]);
+done:
+  free(C);
+  free(rows);
+  if (rc) { free(P->tbl); P->tbl = NULL; }
+  return rc;
+}
+
+static void bench_plan_free(bench_plan *P) {
+  free(P->tbl);
+  free(P->mats);
+}
+
+int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride, uint64_t size,
+                  int nobj, uint8_t *parity, const int *erased, int nerased, int threads,
+                  int force_scalar) {
+  if (k <= 0 || m <= 0 || k + m > 256 || threads <= 0 || nerased > m) return ORC_E_PARAMS;
+  uint64_t bs = orc_block_size(k, 8, size);
+  bench_plan P;
+  int rc = bench_plan_make(&P, op, k, m, erased, nerased);
+  if (rc) return rc;
+  int nout = P.nout;
+  const uint8_t *tbl = P.tbl;
+  const uint64_t *mats = P.mats;
+  const int *want = P.want, *surv = P.surv;
   {
     pthread_t th[256];
     bench_job jobs[256];
@@ -921,8 +958,145 @@ int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
   }
-  free(mats);
-done:
-  free(C); free(rows); free(tbl);
-  return rc;
+  bench_plan_free(&P);
+  return 0;
+}
+
+/* The timed CPU baseline (bench.py cpu_baseline): `threads` workers, worker
+ * t pinned to cpus[t], each copying ITS slice of the sample (objects
+ * [o0, o1) of src) into buffers it allocates and touches itself, so every
+ * page lives on the worker's own NUMA node; then passes of >= pass_s
+ * seconds, each a whole number of rounds of (encode every object, then
+ * decode data blocks `erased` in place) by all workers between two barriers,
+ * until total_s seconds and min_passes passes have run.  rates[i] = GiB/s of
+ * object payload (2 x objects x size per round) of pass i; returns the number
+ * of passes (<= max_passes) or a negative ORC_E_*.  parity_out (nobj x m x
+ * bs) receives the workers' encode of the sample, for the parity check. */
+typedef struct {
+  const uint8_t *src;
+  uint64_t src_stride;
+  int cpu;
+  bench_job enc, dec;
+  uint8_t *objs, *par, *tail;
+  pthread_barrier_t *start, *done;
+  volatile int *stop;
+  int err;
+} pinned_worker;
+
+static void *pinned_main(void *arg) {
+  pinned_worker *W = arg;
+#if defined(__linux__)
+  if (W->cpu >= 0) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(W->cpu, &set);
+    if (pthread_setaffinity_np(pthread_self(), sizeof(set), &set)) W->err = 1;
+  }
+#endif
+  const int n = W->enc.o1 - W->enc.o0;
+  const uint64_t size = W->enc.size, bs = W->enc.bs;
+  const int k = W->enc.k, m = W->enc.m;
+  W->objs = aligned_alloc(64, orc_round_to((uint64_t)(n ? n : 1) * size + 64, 64));
+  W->par = aligned_alloc(64, orc_round_to((uint64_t)(n ? n : 1) * m * bs + 64, 64));
+  W->tail = aligned_alloc(64, orc_round_to(bs * (uint64_t)k + 64, 64));
+  if (!W->objs || !W->par || !W->tail) W->err = 1;
+  else {
+    for (int o = 0; o < n; o++)  /* first touch, by this pinned thread */
+      memcpy(W->objs + (uint64_t)o * size, W->src + (uint64_t)(W->enc.o0 + o) * W->src_stride, size);
+    memset(W->par, 0, (uint64_t)n * m * bs);
+    memset(W->tail, 0, bs * (uint64_t)k);
+  }
+  W->enc.objs = W->dec.objs = W->objs;
+  W->enc.stride = W->dec.stride = size;
+  W->enc.parity = W->dec.parity = W->par;
+  W->enc.o1 = W->dec.o1 = n;
+  W->enc.o0 = W->dec.o0 = 0;
+  for (;;) {
+    pthread_barrier_wait(W->start);
+    if (*W->stop) break;
+    if (!W->err)
+      for (int o = 0; o < n; o++) bench_object(&W->enc, o, W->tail);
+    if (!W->err)
+      for (int o = 0; o < n; o++) bench_object(&W->dec, o, W->tail);
+    pthread_barrier_wait(W->done);
+  }
+  return NULL;
+}
+
+static double now_s(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+int orc_bench_rs8_pinned(int k, int m, const uint8_t *src, uint64_t src_stride, uint64_t size,
+                         int nobj, const int *erased, int nerased, int threads, const int *cpus,
+                         double pass_s, double total_s, int min_passes, double *rates,
+                         int max_passes, uint8_t *parity_out) {
+  if (k <= 0 || m <= 0 || k + m > 256 || threads <= 0 || threads > 256 || nerased > m ||
+      nobj <= 0 || max_passes <= 0)
+    return ORC_E_PARAMS;
+  uint64_t bs = orc_block_size(k, 8, size);
+  bench_plan PE, PD;
+  int rc = bench_plan_make(&PE, 0, k, m, NULL, 0);
+  if (rc) return rc;
+  rc = bench_plan_make(&PD, 1, k, m, erased, nerased);
+  if (rc) { bench_plan_free(&PE); return rc; }
+  const int simd = orc_simd_level();
+  pthread_barrier_t start, done;
+  pthread_barrier_init(&start, NULL, (unsigned)threads + 1);
+  pthread_barrier_init(&done, NULL, (unsigned)threads + 1);
+  volatile int stop = 0;
+  pinned_worker *Ws = calloc((size_t)threads, sizeof(pinned_worker));
+  pthread_t *th = calloc((size_t)threads, sizeof(pthread_t));
+  for (int t = 0; t < threads; t++) {
+    pinned_worker *W = &Ws[t];
+    W->src = src; W->src_stride = src_stride; W->cpu = cpus ? cpus[t] : -1;
+    W->start = &start; W->done = &done; W->stop = &stop;
+    bench_job *E = &W->enc, *D = &W->dec;
+    E->op = 0; E->k = k; E->m = m; E->nout = PE.nout; E->simd = simd; E->size = size; E->bs = bs;
+    E->o0 = (int)((long long)nobj * t / threads);
+    E->o1 = (int)((long long)nobj * (t + 1) / threads);
+    E->tbl = PE.tbl; E->mats = PE.mats; E->want = PE.want; E->surv = PE.surv;
+    *D = *E;
+    D->op = 1; D->nout = PD.nout; D->tbl = PD.tbl; D->mats = PD.mats; D->want = PD.want;
+    D->surv = PD.surv;
+    pthread_create(&th[t], NULL, pinned_main, W);
+  }
+  /* round 0 (untimed): the first touch is done and the caches are warm */
+  pthread_barrier_wait(&start);
+  pthread_barrier_wait(&done);
+  int np = 0;
+  double t_all = 0.0;
+  while (np < max_passes && (t_all < total_s || np < min_passes)) {
+    double t0 = now_s(), dt;
+    int reps = 0;
+    do {
+      pthread_barrier_wait(&start);
+      pthread_barrier_wait(&done);
+      reps++;
+      dt = now_s() - t0;
+    } while (dt < pass_s);
+    t_all += dt;
+    rates[np++] = 2.0 * (double)nobj * (double)size * reps / dt / (double)(1u << 30);
+  }
+  stop = 1;
+  pthread_barrier_wait(&start);
+  int err = 0;
+  for (int t = 0; t < threads; t++) {
+    pthread_join(th[t], NULL);
+    pinned_worker *W = &Ws[t];
+    err |= W->err;
+    const int n = W->enc.o1;
+    if (parity_out && W->par)
+      memcpy(parity_out + (uint64_t)((long long)nobj * t / threads) * m * bs, W->par,
+             (uint64_t)n * m * bs);
+    free(W->objs); free(W->par); free(W->tail);
+  }
+  free(Ws); free(th);
+  pthread_barrier_destroy(&start);
+  pthread_barrier_destroy(&done);
+  bench_plan_free(&PE);
+  bench_plan_free(&PD);
+  return err ? ORC_E_PARAMS : np;
 }

@@ -58,6 +58,11 @@ def lib():
                                                       ctypes.POINTER(ctypes.c_int), ctypes.c_int,
                                                       ctypes.c_uint64, ctypes.POINTER(ctypes.c_int),
                                                       ctypes.c_int, u8p]
+        L.orc_bench_rs8_pinned.argtypes = [
+            ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+            ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_int,
+            ctypes.POINTER(ctypes.c_int), ctypes.c_double, ctypes.c_double, ctypes.c_int,
+            ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_void_p]
         L.orc_bench_rs8.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                     ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
                                     ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
@@ -207,6 +212,26 @@ def bench_rs8(op, k, m, objs, obj_stride, size, nobj, parity, erased=(), threads
     er = (ctypes.c_int * max(len(erased), 1))(*erased)
     _chk(lib().orc_bench_rs8(op, k, m, objs.ctypes.data, obj_stride, size, nobj,
                              parity.ctypes.data, er, len(erased), threads, int(force_scalar)))
+
+
+def bench_rs8_pinned(k, m, objs, size, erased, threads, cpus, pass_s, total_s, min_passes=3,
+                     max_passes=256, parity_out=None):
+    """bench.py's timed CPU baseline: workers pinned to `cpus`, each
+    first-touching its own slice of `objs` (n x stride numpy uint8), passes of
+    >= pass_s seconds of encode + in-place decode of `erased`; returns the
+    per-pass GiB/s (oracle/leoec_oracle.c orc_bench_rs8_pinned)."""
+    L = lib()
+    n, stride = objs.shape[0], objs.strides[0]
+    rates = (ctypes.c_double * max_passes)()
+    er = (ctypes.c_int * max(len(erased), 1))(*erased)
+    cp = (ctypes.c_int * max(len(cpus), 1))(*cpus) if cpus else None
+    po = parity_out.ctypes.data if parity_out is not None else None
+    rc = L.orc_bench_rs8_pinned(k, m, objs.ctypes.data, stride, size, n, er, len(erased), threads,
+                                cp, float(pass_s), float(total_s), min_passes, rates, max_passes,
+                                po)
+    if rc < 0:
+        _chk(rc)
+    return list(rates[:rc])
 
 
 def simd_level():

@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+# glibc writes its fatal-error reports (heap corruption, failed checks) to
+# /dev/tty unless this is set; a GPU box has no tty, so an abort there would
+# otherwise leave no message (round 2's unexplained abort).
+os.environ.setdefault("LIBC_FATAL_STDERR_", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

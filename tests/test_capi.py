@@ -129,3 +129,5 @@ def test_no_cpu_fallback_without_gpu(le):
     st, why = le.nif_encode("vandrs", (10, 4, 8), b"x" * 5000, 5000)
     assert (st, why) == ("error", "No gfx950 HIP device")
     assert le.gf_init() == ("error", "No gfx950 HIP device")
+    assert le._lib.lib.leoec_host_lanes(None, 0) == le._lib.E_NO_DEVICE
+    assert le._lib.lib.leoec_device() == le._lib.E_NO_DEVICE

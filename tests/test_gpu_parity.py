@@ -269,6 +269,8 @@ def test_device_roundtrip_bench_shape(gpu, le):
                                  {"LEOEC_GFBIT_FORM": "1", "LEOEC_GFBIT_PF": "0"},
                                  {"LEOEC_GFBIT_FORM": "1", "LEOEC_GFBIT_LW": "1"},
                                  {"LEOEC_GFBIT_WG": "128"},
+                                 {"LEOEC_GFBIT_WG": "128", "LEOEC_GFBIT_PF": "0"},
+                                 {"LEOEC_GFBIT_LW": "4", "LEOEC_GFBIT_PF": "0"},
                                  {"LEOEC_GFBIT_FORM": "1", "LEOEC_GFBIT_WG": "128"},
                                  {"LEOEC_GFBIT_WAVES": "4"}, {"LEOEC_GFBIT_WAVES": "5"},
                                  {"LEOEC_GFBIT_FORM": "2"}],  # gfbx_apply (LDS-shared, split rows)
@@ -728,7 +730,8 @@ def _capi_roundtrip(le, c, t):
     return None
 
 
-@pytest.mark.parametrize("form", ["product", "always-batch", "per-thread"])
+@pytest.mark.parametrize("form", ["product", "always-batch", "per-thread", "lanes4",
+                                  "lanes4-always-batch", "fail-one"])
 def test_host_batching_mixed_callers(gpu, le, oracle, form, request):
     """Cross-call batching (hostq.cpp): 24 threads call the C ABI at once with
     mixed classes, widths, sizes (ragged, and 9 MiB objects above the batch
@@ -736,17 +739,29 @@ def test_host_batching_mixed_callers(gpu, le, oracle, form, request):
     holds several different maps (several launches) and identical maps are
     merged into one launch.  Every result equals the oracle's.  The
     measurement build forces every call through the queue (always-batch) or
-    none (per-thread) and reports how calls were batched."""
+    none (per-thread) and reports how calls were batched; "lanes4" runs the
+    node dispatcher with 4 lanes (queues) mapped onto the box's device(s),
+    every lane carrying jobs; "fail-one" makes the batched launches of one
+    spec report a HIP error: exactly those calls fail, every other call in
+    the same batches succeeds bit-exact."""
     import concurrent.futures as cf
-    stats = None
+    stats = lane_jobs = None
+    fail_bs = None
     if form != "product":
         ms = request.getfixturevalue("measure")
-        if form == "always-batch":
+        if form in ("always-batch", "lanes4-always-batch", "fail-one"):
             ms.setenv("LEOEC_HOSTQ_DIRECT", "0")
             ms.setenv("LEOEC_HOSTQ_DIRECT_MAP", "0")
-        else:
+        if form == "per-thread":
             ms.setenv("LEOEC_HOST_BATCH", "0")
+        if form.startswith("lanes4"):
+            ms.setenv("LEOEC_HOSTQ_LANES", "4")
+            assert len(le._lib.host_lanes()) == 4
+        if form == "fail-one":
+            fail_bs = 1296  # cauchyrs(4,2,3) on 5000 B: bs = ceil16(5000 / 12) * 3
+            ms.setenv("LEOEC_HOSTQ_FAIL_BS", str(fail_bs))
         stats = le._lib._current.leoec_measure_hostq_stats
+        lane_jobs = le._lib._current.leoec_measure_hostq_lane_jobs
     specs = [("vandrs", 10, 4, 8, 1048576), ("vandrs", 10, 4, 8, 1048576),
              ("vandrs", 10, 4, 8, 300001), ("cauchyrs", 10, 4, 8, 1048576 + 77),
              ("isars", 10, 4, 8, 65536 + 7), ("liberation", 4, 2, 7, 777777),
@@ -756,12 +771,22 @@ def test_host_batching_mixed_callers(gpu, le, oracle, form, request):
     cases = [_capi_case(le, oracle, *sp, seed=100 + i) for i, sp in enumerate(specs)]
     import ctypes
     buf = (ctypes.c_double * 14)()
+    lanes = (ctypes.c_double * 64)()
     if stats:
         stats(buf)
+        lane_jobs(lanes)
 
     def worker(t):
+        failed = 0
         for r in range(8):
-            e = _capi_roundtrip(le, cases[(t + r) % len(cases)], t + r)
+            c = cases[(t + r) % len(cases)]
+            e = _capi_roundtrip(le, c, t + r)
+            if fail_bs is not None and c["bs"] == fail_bs:
+                # the injected failure: the encode reports the HIP error
+                if not (e and e.startswith("encode") and e.endswith(f"rc {le._lib.E_HIP}")):
+                    return f"thread {t}: expected an injected failure, got {e}"
+                failed += 1
+                continue
             if e:
                 return f"thread {t}: {e}"
         return None
@@ -771,9 +796,14 @@ def test_host_batching_mixed_callers(gpu, le, oracle, form, request):
     assert not errs, errs
     if stats:
         stats(buf)
+        lane_jobs(lanes)
         batches, jobs, launches = buf[0], buf[1], buf[2]
-        if form == "always-batch":
+        if form in ("always-batch", "lanes4-always-batch"):
             # 24 x 8 x 3 calls, minus the 9 MiB ones (per-thread path)
             assert jobs >= 24 * 8 * 3 * 0.8 and batches < jobs and launches > batches, list(buf)
-        else:
+        elif form == "per-thread":
             assert batches == 0, list(buf)
+        if form.startswith("lanes4"):
+            assert sum(1 for x in lanes[:4] if x > 0) >= (4 if "always" in form else 2), \
+                list(lanes[:4])
+            assert sum(lanes[4:]) == 0

@@ -21,6 +21,7 @@ def maps(tmp_path_factory):
                     os.path.join(HERE, "tile_maps_test.cpp"), "-o", so], check=True)
     L = ctypes.CDLL(so)
     L.tile_map_image.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+    L.packet_lane_check.argtypes = [ctypes.c_uint32] * 6
     return L
 
 
@@ -64,3 +65,36 @@ def test_xcd_obj_map_is_a_permutation(maps, nobj, tiles, run):
         xcd_of[m] = np.arange(n) % 8
         per_obj = xcd_of[: (full // tiles) * tiles].reshape(-1, tiles)
         assert np.all(per_obj == per_obj[:, :1])
+
+
+def _bs(size, k, w):
+    """leo_erasure's block size: ceil16(ceil(size / (k w))) w (common.cpp:24)."""
+    return -(-(-(-size // (k * w))) // 16) * 16 * w
+
+
+# (WG lanes, bytes per lane) of every gfbit_apply / gfb2_apply launch form:
+# shipped 256 x 8 (w <= 11) and 256 x 4 (w >= 12); measurement forms 256 x 16,
+# 128 x 16 (both look-ahead settings, including the one that aborted in round
+# 2), 64 x 8
+PACKET_FORMS = [(256, 8), (256, 4), (256, 16), (128, 16), (64, 8)]
+
+
+@pytest.mark.parametrize("wg,lb", PACKET_FORMS)
+def test_packet_lane_geometry(maps, wg, lb):
+    """Every packet-kernel launch shape of the parity tests and the BASELINE
+    configs: cauchyrs(10,4,8) at 1 MiB (ps 13,120, packets start mid line) and
+    100,003 B (the round-2 abort's first call), (6,3,4), (4,2,3), every w of
+    gfbit (2..16) on ragged sizes; data blocks full, partial (the tail block)
+    and empty, output blocks full and clipped."""
+    cases = [(1048576, 10, 8), (100003, 10, 8), (100003, 6, 4), (100003, 4, 3),
+             (1054720, 10, 8), (1, 10, 8), (4097, 4, 3)]
+    cases += [(150001, 5, w) for w in range(2, 17)]
+    for size, k, w in cases:
+        bs = _bs(size, k, w)
+        tail = size - (k - 1) * bs if size > (k - 1) * bs else 0
+        for vin in sorted({bs, max(tail, 0), 0, 1, bs - 1, bs // 2 + 3}):
+            for vout in sorted({bs, vin}):
+                if vin > bs or vout > bs:
+                    continue
+                rc = maps.packet_lane_check(bs, w, wg, lb, vin, vout)
+                assert rc == 0, (size, k, w, bs, vin, vout, rc)

@@ -37,4 +37,21 @@ if [[ $STEPS == *prof* ]]; then
       python "$ROOT/bench.py" --steps 10 --no-cpu
   cd "$ROOT"
 fi
+if [[ $STEPS == *pmc* ]]; then
+  # HBM bytes of the bench kernel: FETCH_SIZE and WRITE_SIZE in separate
+  # passes (TCC slots), 1 MiB x 2048 and configs[4]'s 64 x 64 MiB; the JSON
+  # records are stamped with the gf8_apply<10,4> code object they ran on
+  cd /tmp && export TMPDIR=/tmp
+  for wl in 1MiB 64MiB; do
+    for c in FETCH_SIZE WRITE_SIZE; do
+      run pmc_${wl}_$c 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_${wl}_$c" -o run -- \
+          python "$ROOT/bench.py" --workload $wl --steps 3 --warmup 1 --warmup-s 0 --no-cpu
+    done
+  done
+  cd "$ROOT"
+  python tools/pmc_traffic.py "$OUT" --fetch pmc_1MiB_FETCH_SIZE --write pmc_1MiB_WRITE_SIZE \
+      > "$OUT/pmc_traffic.json"
+  python tools/pmc_traffic.py "$OUT" --objects 64 --object-bytes 67108864 \
+      --fetch pmc_64MiB_FETCH_SIZE --write pmc_64MiB_WRITE_SIZE > "$OUT/pmc_traffic_64MiB.json"
+fi
 echo "session done"

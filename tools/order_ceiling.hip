@@ -166,7 +166,7 @@ int main(int argc, char** argv) {
     cases.push_back({"object-major" + w, wg, 1, 1});
     cases.push_back({"xcd objects" + w, wg, 3, 1});
     cases.push_back({"xcd segments" + w, wg, 4, 1});
-    for (unsigned c : {8u, 26u, 64u, 256u, 1024u}) {
+    for (unsigned c : {8u, 26u, 64u, 128u, 256u, 512u, 1024u}) {
       cases.push_back({"chunked C" + std::to_string(c) + w, wg, 2, c});
       cases.push_back({"xcd chunked C" + std::to_string(c) + w, wg, 5, c});
     }
