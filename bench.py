@@ -168,13 +168,43 @@ def _cpu_list(text):
     return out
 
 
-def pick_cpus(threads, sysfs="/sys/devices/system"):
+def _cpu_busy(window_s=0.25):
+    """Fraction of time each CPU was busy over a short window (/proc/stat),
+    or {} where /proc/stat is unreadable."""
+    def snap():
+        out = {}
+        try:
+            with open("/proc/stat") as fh:
+                for line in fh:
+                    f = line.split()
+                    if f and f[0].startswith("cpu") and f[0] != "cpu":
+                        v = [int(x) for x in f[1:]]
+                        out[int(f[0][3:])] = (sum(v), v[3] + (v[4] if len(v) > 4 else 0))
+        except (OSError, ValueError):
+            return {}
+        return out
+    a = snap()
+    time.sleep(window_s)
+    b = snap()
+    busy = {}
+    for c in a.keys() & b.keys():
+        tot, idle = b[c][0] - a[c][0], b[c][1] - a[c][1]
+        busy[c] = 1.0 - idle / tot if tot > 0 else 0.0
+    return busy
+
+
+def pick_cpus(threads, sysfs="/sys/devices/system", busy=None):
     """CPUs to pin the baseline's `threads` workers to: one hardware thread
-    per physical core (no two workers on SMT siblings), from the NUMA node
-    this process runs on first, then the other nodes, within the affinity
-    mask (the cgroup's cpuset).  Returns (cpus, {numa nodes used})."""
+    per physical core (no two workers on SMT siblings), all on one NUMA node
+    where it has enough cores, within the affinity mask (the cgroup's
+    cpuset).  The host is shared with other tenants, so the cores are the
+    least busy ones over a short /proc/stat window (a core counts as busy as
+    its busiest sibling), and the node is the one whose `threads` least busy
+    cores are idlest.  Returns (cpus, {numa nodes used})."""
     aff = sorted(os.sched_getaffinity(0))
     allowed = set(aff)
+    if busy is None:
+        busy = _cpu_busy()
 
     def read(path):
         try:
@@ -190,25 +220,41 @@ def pick_cpus(threads, sysfs="/sys/devices/system"):
             continue
         for c in _cpu_list(t):
             node_of[c] = nd
-    try:
-        import ctypes
-        here = ctypes.CDLL(None).sched_getcpu()
-    except (OSError, AttributeError):
-        here = aff[0]
-    home = node_of.get(here, 0)
-    seen_cores, first, rest = set(), [], []
+    cores = {}  # physical core -> (its allowed cpus, busiest sibling's load)
     for c in aff:
         sib = read(f"{sysfs}/cpu/cpu{c}/topology/thread_siblings_list")
-        core = min(_cpu_list(sib)) if sib else c
-        if core in seen_cores:
-            continue
-        seen_cores.add(core)
-        (first if node_of.get(c, 0) == home else rest).append(c)
-    cpus = (first + rest)[:threads]
+        sibs = _cpu_list(sib) if sib else [c]
+        core = min(sibs)
+        load = max(busy.get(x, 0.0) for x in sibs)
+        cpu_list, _ = cores.get(core, ([], 0.0))
+        cores[core] = (cpu_list + [c], load)
+    by_node = {}
+    for core, (cl, load) in cores.items():
+        by_node.setdefault(node_of.get(cl[0], 0), []).append((load, cl[0]))
+    for v in by_node.values():
+        v.sort()
+    full = [nd for nd, v in by_node.items() if len(v) >= threads]
+    if full:  # the node whose `threads` least busy cores are idlest
+        nd = min(full, key=lambda n: (sum(x for x, _ in by_node[n][:threads]), n))
+        cpus = [c for _, c in by_node[nd][:threads]]
+    else:  # no node has enough cores: the least busy cores anywhere
+        cpus = [c for _, c in sorted(x for v in by_node.values() for x in v)][:threads]
     if len(cpus) < threads:  # fewer physical cores than threads: reuse siblings
         cpus += [c for c in aff if c not in cpus][: threads - len(cpus)]
     cpus = [c for c in cpus if c in allowed]
     return cpus, sorted({node_of.get(c, 0) for c in cpus})
+
+
+def _cgroup_throttled_us():
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as fh:
+            for line in fh:
+                k, _, v = line.partition(" ")
+                if k == "throttled_usec":
+                    return int(v)
+    except (OSError, ValueError):
+        pass
+    return None
 
 
 def cpu_baseline(objs, parity, size, n_sample, target_s):
@@ -235,10 +281,12 @@ def cpu_baseline(objs, parity, size, n_sample, target_s):
     # barriers); value = the median pass.  cpu_par receives the workers'
     # encode of the sample, compared with the GPU's parity after the clock.
     pass_s = target_s / 12.0
+    thr0 = _cgroup_throttled_us()
     t0 = time.perf_counter()
     rates = O.bench_rs8_pinned(K, M, host, size, ERASED, threads, cpus, pass_s, target_s,
                                min_passes=3, parity_out=cpu_par)
     t_all = time.perf_counter() - t0
+    thr1 = _cgroup_throttled_us()
     parity_ok = bool(np.array_equal(cpu_par, gpu_par))
     rates.sort()
     med = rates[len(rates) // 2]
@@ -251,7 +299,10 @@ def cpu_baseline(objs, parity, size, n_sample, target_s):
                   f"vandrs RS({K},{M},8) encode + in-place decode of data blocks {ERASED}, "
                   f"{threads} threads pinned one per physical core, each first-touching its "
                   f"own slice, {t_all:.2f} s; value = median pass",
-        "pinning": {"cpus": cpus, "numa_nodes": nodes, "first_touch": "per worker thread"},
+        "pinning": {"cpus": cpus, "numa_nodes": nodes, "first_touch": "per worker thread",
+                    "choice": "least busy physical cores of one NUMA node (/proc/stat)"},
+        "cgroup_throttled_s": None if thr0 is None or thr1 is None else
+        round((thr1 - thr0) / 1e6, 3),
         "pass_spread": round((rates[-1] - rates[0]) / med, 4) if med else None,
         "iqr_spread": round((rates[(3 * len(rates)) // 4] - rates[len(rates) // 4]) / med, 4)
         if med else None,

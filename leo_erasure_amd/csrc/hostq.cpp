@@ -73,6 +73,8 @@ struct Slot {
   uint8_t* d_out = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
+  hipEvent_t ev_blk = nullptr;  // the same, created hipEventBlockingSync (Knobs::hostq_sync = 2)
+  hipEvent_t ev_done = nullptr; // the one recorded for this batch (ev or ev_blk)
   hipEvent_t ev_h2d = nullptr;  // after the input copy: the H2D engine is free for the next batch
   uint64_t used_in = 0, used_out = 0;
   std::vector<const HostJob*> jobs;
@@ -99,8 +101,9 @@ struct Queue {
   int direct = 0;              // calls on their per-thread path (HostqTicket)
 };
 
-// Wait for `ev` without holding the queue lock: hipEventSynchronize, or
-// (Knobs::hostq_sync = 1, measurement) a hipEventQuery poll with yields.
+// Wait for `ev` without holding the queue lock: (Knobs::hostq_sync = 1) a
+// hipEventQuery poll with yields, else hipEventSynchronize (= 2: on an event
+// created hipEventBlockingSync, which sleeps instead of spinning).
 hipError_t wait_event(hipEvent_t ev) {
   if (knobs().hostq_sync == 1) {
     for (;;) {
@@ -119,6 +122,8 @@ int slot_alloc(Slot* s) {
       hipMalloc((void**)&s->d_out, kSlotBytes) != hipSuccess ||
       hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&s->ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_blk, hipEventDisableTiming | hipEventBlockingSync) !=
+          hipSuccess ||
       hipEventCreateWithFlags(&s->ev_h2d, hipEventDisableTiming) != hipSuccess) {
     if (s->h_in) (void)hipHostFree(s->h_in);
     if (s->h_out) (void)hipHostFree(s->h_out);
@@ -193,7 +198,8 @@ int launch_slot(Slot* s) {
           hipSuccess)
     rc = LEOEC_E_HIP;
   stat_add(13, us_since(t));
-  if (hipEventRecord(s->ev, s->stream) != hipSuccess) {
+  s->ev_done = knobs().hostq_sync == 2 ? s->ev_blk : s->ev;
+  if (hipEventRecord(s->ev_done, s->stream) != hipSuccess) {
     (void)hipStreamSynchronize(s->stream);  // no event to wait on: drain here
     if (rc == LEOEC_OK) rc = LEOEC_E_HIP;
   }
@@ -270,7 +276,7 @@ void completer_main(Queue* q) {
     Slot* s = q->inflight.front();
     lk.unlock();
     const Clock::time_point tw = Clock::now();
-    const int rc = wait_event(s->ev) == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
+    const int rc = wait_event(s->ev_done) == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
     stat_add(5, us_since(tw));
     lk.lock();
     s->done = Clock::now();

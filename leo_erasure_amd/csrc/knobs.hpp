@@ -20,7 +20,7 @@ struct Knobs {
   int batch_window_us = 0;   // LEOEC_BATCH_WINDOW_US: hold an idle-GPU batch open this long
   int hostq_depth = 3;       // LEOEC_HOSTQ_DEPTH: batches on the GPU at once
   int hostq_sync = 1;        // LEOEC_HOSTQ_SYNC: 1 poll events (hipEventQuery + yield),
-                             //   0 hipEventSynchronize
+                             //   0 hipEventSynchronize, 2 the same on blocking-sync events
   int hostq_close = 1;       // LEOEC_HOSTQ_CLOSE: 1 close a batch when the previous H2D is
                              //   done, 0 as soon as the GPU has room
   int hostq_direct = 4;      // LEOEC_HOSTQ_DIRECT: encode calls that may take the per-thread

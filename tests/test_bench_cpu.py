@@ -1,0 +1,73 @@
+"""bench.py's CPU-baseline placement (CPU only): workers go one per physical
+core, on one NUMA node, on the least busy cores of a shared host; and the
+pinned, first-touch timed baseline reproduces the oracle's parity."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def _fake_sysfs(tmp_path, nodes, smt):
+    """nodes x cores-per-node x smt hardware threads; cpu id = sibling-major
+    (cpu c and c + ncores are siblings, as on the MI355X boxes' EPYC hosts)."""
+    per, n = nodes[0], len(nodes)
+    ncores = per * n
+    for nd in range(n):
+        cpus = [c for c in range(ncores * smt) if (c % ncores) // per == nd]
+        d = tmp_path / "node" / f"node{nd}"
+        d.mkdir(parents=True)
+        (d / "cpulist").write_text(",".join(map(str, cpus)))
+    for c in range(ncores * smt):
+        d = tmp_path / "cpu" / f"cpu{c}" / "topology"
+        d.mkdir(parents=True)
+        sib = [c % ncores + i * ncores for i in range(smt)]
+        (d / "thread_siblings_list").write_text(",".join(map(str, sib)))
+    return str(tmp_path)
+
+
+def test_one_worker_per_core_on_one_node(tmp_path, monkeypatch):
+    sysfs = _fake_sysfs(tmp_path, [8, 8], 2)  # 2 nodes x 8 cores x 2 threads = 32 cpus
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(32)))
+    busy = {c: 0.0 for c in range(32)}
+    for c in range(0, 8):  # node 0 busy (another tenant)
+        busy[c] = 0.9
+    cpus, nodes = bench.pick_cpus(6, sysfs=sysfs, busy=busy)
+    assert nodes == [1] and len(cpus) == 6
+    cores = {c % 16 for c in cpus}
+    assert len(cores) == 6  # no two workers on SMT siblings
+    assert all(8 <= c % 16 < 16 for c in cpus)
+
+
+def test_busy_sibling_makes_the_core_busy(tmp_path, monkeypatch):
+    sysfs = _fake_sysfs(tmp_path, [4], 2)  # one node, 4 cores, cpus 0-7
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(8)))
+    busy = {c: 0.0 for c in range(8)}
+    busy[4] = 1.0  # sibling of cpu 0
+    cpus, _ = bench.pick_cpus(3, sysfs=sysfs, busy=busy)
+    assert 0 not in cpus and 4 not in cpus and len(cpus) == 3
+
+
+def test_more_threads_than_cores_of_a_node(tmp_path, monkeypatch):
+    sysfs = _fake_sysfs(tmp_path, [4, 4], 1)
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(8)))
+    cpus, nodes = bench.pick_cpus(6, sysfs=sysfs, busy={})
+    assert len(set(cpus)) == 6 and nodes == [0, 1]
+
+
+def test_pinned_baseline_parity(oracle):
+    n, size = 24, 300001
+    objs = np.random.default_rng(7).integers(0, 256, (n, size), dtype=np.uint8)
+    bs = oracle.block_size(10, 8, size)
+    par = np.zeros((n, 4 * bs), np.uint8)
+    ref = np.zeros_like(par)
+    cpus, _ = bench.pick_cpus(3)
+    rates = oracle.bench_rs8_pinned(10, 4, objs, size, [0, 1, 2, 3], 3, cpus, 0.05, 0.2,
+                                    parity_out=par)
+    oracle.bench_rs8(0, 10, 4, objs, size, size, n, ref, threads=2)
+    assert len(rates) >= 3 and all(r > 0 for r in rates)
+    assert np.array_equal(par, ref)

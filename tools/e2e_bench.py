@@ -63,8 +63,11 @@ def callers(le, T, per, op, bs, filled, tag):
     stats = getattr(le._lib._current, "leoec_measure_hostq_stats", None)
     buf = (ctypes.c_double * 14)()
 
+    cpu = []
+
     def trial():
-        """All T threads call back to back for `per` seconds; calls/s."""
+        """All T threads call back to back for `per` seconds; calls/s (and
+        the process's CPU time over the trial, in cores)."""
         ready = threading.Barrier(T + 1)
         go = threading.Event()
         counts = [0] * T
@@ -86,12 +89,15 @@ def callers(le, T, per, op, bs, filled, tag):
         for th in ths:
             th.start()
         ready.wait()
+        c0 = time.process_time()
         t0 = time.perf_counter()
         box["end"] = t0 + per
         go.set()
         for th in ths:
             th.join()
-        return sum(counts), time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        cpu.append((time.process_time() - c0) / dt)
+        return sum(counts), dt
 
     trial()  # warm-up trial (first use of the queue's slots)
     if stats:
@@ -106,7 +112,8 @@ def callers(le, T, per, op, bs, filled, tag):
     dt = sum(d for _, d in runs)
     rec = {"path": f"C ABI leoec_{op}, 1 MiB objects, {T} caller threads [{tag}]",
            "GiBps": round(rates[1], 2), "GiBps_min_max": [round(rates[0], 2), round(rates[-1], 2)],
-           "us_per_call": round(dt * T / calls * 1e6, 1), "calls": calls}
+           "us_per_call": round(dt * T / calls * 1e6, 1), "calls": calls,
+           "cpu_cores": round(sorted(cpu[1:])[len(cpu[1:]) // 2], 2)}
     if stats:
         stats(buf)
         nb, nj = buf[0], buf[1]
@@ -190,7 +197,16 @@ def main():
     assert le.gf_init() == "ok"
     bs, filled = le.layout("vandrs", (K, M, W), SIZE)
     quick = "--quick" in sys.argv
-    if "--queue-ab" in sys.argv:  # batching-queue policies (hostq.cpp knobs)
+    if "--forms" in sys.argv:  # --forms "tag:K=V,K=V;tag2:..." [--threads 1,8,32]
+        spec = sys.argv[sys.argv.index("--forms") + 1]
+        forms = []
+        for ent in spec.split(";"):
+            tag, _, kv = ent.partition(":")
+            forms.append((tag, dict(x.split("=", 1) for x in kv.split(",") if x)))
+        threads, with_mirror = (1, 8, 32), False
+        if "--threads" in sys.argv:
+            threads = tuple(int(x) for x in sys.argv[sys.argv.index("--threads") + 1].split(","))
+    elif "--queue-ab" in sys.argv:  # batching-queue policies (hostq.cpp knobs)
         # default: close when the previous H2D is done, poll events, depth 3
         # default: idle queue -> up to 4 calls direct, else batched; a batch
         # closes when the previous H2D is done; events polled; depth 3

@@ -30,6 +30,7 @@ run() {  # name timeout cmd...
 [[ $STEPS == *test* ]] && run pytest 1200 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}
 [[ $STEPS == *bench1* ]] && run bench 600 python bench.py ${BENCH_ARGS:-}
 [[ $STEPS == *bench2* ]] && run bench2 600 python bench.py --gpus 2 --oversubscribe --steps 50 --warmup 10
+[[ $STEPS == *e2e* ]] && run e2e 900 python tools/e2e_bench.py ${E2E_ARGS:---quick}
 [[ $STEPS == *bench64* ]] && run bench64 600 python bench.py --workload 64MiB --steps 50 --warmup 10 --no-cpu
 if [[ $STEPS == *prof* ]]; then
   cd /tmp && export TMPDIR=/tmp
