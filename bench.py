@@ -168,29 +168,35 @@ def _cpu_list(text):
     return out
 
 
-def _cpu_busy(window_s=0.25):
-    """Fraction of time each CPU was busy over a short window (/proc/stat),
-    or {} where /proc/stat is unreadable."""
-    def snap():
-        out = {}
-        try:
-            with open("/proc/stat") as fh:
-                for line in fh:
-                    f = line.split()
-                    if f and f[0].startswith("cpu") and f[0] != "cpu":
-                        v = [int(x) for x in f[1:]]
-                        out[int(f[0][3:])] = (sum(v), v[3] + (v[4] if len(v) > 4 else 0))
-        except (OSError, ValueError):
-            return {}
-        return out
-    a = snap()
-    time.sleep(window_s)
-    b = snap()
+def _cpu_snap():
+    """{cpu: (total jiffies, idle jiffies)} from /proc/stat, {} if unreadable."""
+    out = {}
+    try:
+        with open("/proc/stat") as fh:
+            for line in fh:
+                f = line.split()
+                if f and f[0].startswith("cpu") and f[0] != "cpu":
+                    v = [int(x) for x in f[1:]]
+                    out[int(f[0][3:])] = (sum(v), v[3] + (v[4] if len(v) > 4 else 0))
+    except (OSError, ValueError):
+        return {}
+    return out
+
+
+def _busy_between(a, b):
     busy = {}
     for c in a.keys() & b.keys():
         tot, idle = b[c][0] - a[c][0], b[c][1] - a[c][1]
         busy[c] = 1.0 - idle / tot if tot > 0 else 0.0
     return busy
+
+
+def _cpu_busy(window_s=0.25):
+    """Fraction of time each CPU was busy over a short window (/proc/stat),
+    or {} where /proc/stat is unreadable."""
+    a = _cpu_snap()
+    time.sleep(window_s)
+    return _busy_between(a, _cpu_snap())
 
 
 def pick_cpus(threads, sysfs="/sys/devices/system", busy=None):
@@ -282,11 +288,14 @@ def cpu_baseline(objs, parity, size, n_sample, target_s):
     # encode of the sample, compared with the GPU's parity after the clock.
     pass_s = target_s / 12.0
     thr0 = _cgroup_throttled_us()
+    snap0 = _cpu_snap()
     t0 = time.perf_counter()
     rates = O.bench_rs8_pinned(K, M, host, size, ERASED, threads, cpus, pass_s, target_s,
                                min_passes=3, parity_out=cpu_par)
     t_all = time.perf_counter() - t0
+    busy = _busy_between(snap0, _cpu_snap())
     thr1 = _cgroup_throttled_us()
+    passes = [round(r, 2) for r in rates]
     parity_ok = bool(np.array_equal(cpu_par, gpu_par))
     rates.sort()
     med = rates[len(rates) // 2]
@@ -303,6 +312,10 @@ def cpu_baseline(objs, parity, size, n_sample, target_s):
                     "choice": "least busy physical cores of one NUMA node (/proc/stat)"},
         "cgroup_throttled_s": None if thr0 is None or thr1 is None else
         round((thr1 - thr0) / 1e6, 3),
+        "passes_GiBps": passes,
+        # the host is shared: CPUs busy during the baseline, ours included
+        # (the workers' `threads`), as a record of the other tenants' load
+        "host_busy_cpus": round(sum(busy.values()), 1) if busy else None,
         "pass_spread": round((rates[-1] - rates[0]) / med, 4) if med else None,
         "iqr_spread": round((rates[(3 * len(rates)) // 4] - rates[len(rates) // 4]) / med, 4)
         if med else None,

@@ -64,7 +64,8 @@ def _load(path=LIB_PATH):
     L.leoec_version.restype = ctypes.c_char_p
     L.leoec_gf_init.argtypes = []
     L.leoec_device.argtypes = []
-    L.leoec_host_lanes.argtypes = [ctypes.POINTER(c_int), c_int]
+    if hasattr(L, "leoec_host_lanes"):  # (absent from pre-round-3 builds, A/B tools)
+        L.leoec_host_lanes.argtypes = [ctypes.POINTER(c_int), c_int]
     L.leoec_check_params.argtypes = [c_int] * 4
     L.leoec_layout.argtypes = [c_int] * 4 + [u64, ctypes.POINTER(u64), ctypes.POINTER(c_int)]
     L.leoec_encode.argtypes = [c_int] * 4 + [u8p, u64, u8p, u64]

@@ -197,6 +197,21 @@ def main():
     assert le.gf_init() == "ok"
     bs, filled = le.layout("vandrs", (K, M, W), SIZE)
     quick = "--quick" in sys.argv
+    if "--libs" in sys.argv:  # --libs "tag:path;tag2:path2" [--threads ..] [--rounds R]
+        # libraries A/B in one process, interleaved rounds (no knobs)
+        libs = [e.partition(":")[::2] for e in sys.argv[sys.argv.index("--libs") + 1].split(";")]
+        threads = (1, 8, 32)
+        if "--threads" in sys.argv:
+            threads = tuple(int(x) for x in sys.argv[sys.argv.index("--threads") + 1].split(","))
+        rounds = int(sys.argv[sys.argv.index("--rounds") + 1]) if "--rounds" in sys.argv else 2
+        for r in range(rounds):
+            for tag, path in libs:
+                le._lib.use_library(path)
+                assert le.gf_init() == "ok"
+                for op in ("encode", "decode"):
+                    for T in threads:
+                        callers(le, T, 0.4, op, bs, filled, f"{tag} round {r}")
+        return
     if "--forms" in sys.argv:  # --forms "tag:K=V,K=V;tag2:..." [--threads 1,8,32]
         spec = sys.argv[sys.argv.index("--forms") + 1]
         forms = []
