@@ -221,7 +221,9 @@ int device_cus() {
   }();
   return cus;
 }
+#ifdef LEOEC_MEASURE
 int gfp_blocks_per_cu() { return knobs().gfp_bpc; }
+#endif
 // Knobs::gf8_tmap: gf8_apply workgroup -> tile order (Gf8Args::tmap), A/B only.
 int gf8_tile_map() { return knobs().gf8_tmap; }
 int gf8_wg_env() { return knobs().gf8_wg; }

@@ -104,6 +104,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--skip-cpu", action="store_true")
+    ap.add_argument("--variants", action="store_true", help="also the cauchyrs A/B forms")
     args = ap.parse_args()
     import torch
 
@@ -121,20 +122,22 @@ def main():
                 "cfg1/2: vandrs RS(10,4,8) 1 MiB x1024", layout="stripe")
     stripe_case(torch, le, "cauchyrs", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], [0, 5, 10, 13],
                 "cfg3: cauchyrs(10,4,8) bitmatrix 1 MiB x1024")
-    for env, label in [({"LEOEC_GFBIT_LW": "1"}, "lane 4 B"), ({"LEOEC_GFBIT_LW": "4"}, "lane 16 B"),
-                       ({"LEOEC_BITMATRIX": "1"}, "masked bitmatrix kernel")]:
-        os.environ.update(env)
-        le._lib.measure_reload()  # knobs live in the measurement build
-        stripe_case(torch, le, "cauchyrs", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], None,
-                    "cfg3 variant (%s): cauchyrs(10,4,8) 1 MiB x1024" % label)
-        for k in env:
-            os.environ.pop(k)
+    if args.variants:
+        for env, label in [({"LEOEC_GFBIT_LW": "1"}, "lane 4 B"),
+                           ({"LEOEC_GFBIT_LW": "4"}, "lane 16 B"),
+                           ({"LEOEC_BITMATRIX": "1"}, "masked bitmatrix kernel")]:
+            os.environ.update(env)
             le._lib.measure_reload()  # knobs live in the measurement build
-    stripe_case(torch, le, "vandrs", 10, 4, 8, 64 * MiB, 16, R, [0, 1, 2, 3], None,
-                "cfg4: vandrs RS(10,4,8) 64 MiB x16 per GPU")
-    stripe_case(torch, le, "isars", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], None,
+            stripe_case(torch, le, "cauchyrs", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], None,
+                        "cfg3 variant (%s): cauchyrs(10,4,8) 1 MiB x1024" % label)
+            for k in env:
+                os.environ.pop(k)
+                le._lib.measure_reload()
+    stripe_case(torch, le, "vandrs", 10, 4, 8, 64 * MiB, 64, R, [0, 1, 2, 3], None,
+                "cfg4: vandrs RS(10,4,8) 64 MiB x64 per GPU")
+    stripe_case(torch, le, "isars", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], [0, 5, 10, 13],
                 "isars(10,4,8) 1 MiB x1024")
-    stripe_case(torch, le, "liberation", 7, 2, 7, MiB, 1024, R, [0, 1], None,
+    stripe_case(torch, le, "liberation", 7, 2, 7, MiB, 1024, R, [0, 1], [0, 7],
                 "liberation(7,2,7) 1 MiB x1024")
     stripe_case(torch, le, "liberation", 4, 2, 7, MiB, 1024, R, [0, 1], None,
                 "liberation(4,2,7) 1 MiB x1024")
@@ -142,17 +145,24 @@ def main():
                 "liberation(10,2,11) 1 MiB x1024")
     stripe_case(torch, le, "vandrs", 10, 4, 8, 16 * MiB, 64, R, [0, 1, 2, 3], None,
                 "vandrs RS(10,4,8) 16 MiB x64")
-    stripe_case(torch, le, "vandrs", 10, 4, 16, MiB, 512, R, [0, 1, 2, 3], None,
-                "vandrs RS(10,4,16) 1 MiB x512")
-    stripe_case(torch, le, "vandrs", 10, 4, 32, MiB, 256, R, [0, 1, 2, 3], None,
-                "vandrs RS(10,4,32) 1 MiB x256")
+    stripe_case(torch, le, "vandrs", 10, 4, 16, MiB, 1024, R, [0, 1, 2, 3], None,
+                "vandrs RS(10,4,16) 1 MiB x1024")
+    stripe_case(torch, le, "vandrs", 10, 4, 32, MiB, 1024, R, [0, 1, 2, 3], None,
+                "vandrs RS(10,4,32) 1 MiB x1024")
     if not args.skip_cpu:
         import bench
-        threads = min(16, len(os.sched_getaffinity(0)))
-        # config 0 of BASELINE.json: RS(4,2,8) 1 MiB encode+decode on the CPU
+        # config 0 of BASELINE.json: RS(4,2,8) 1 MiB encode+decode on the CPU,
+        # bench.py's baseline (pinned, first-touch, median pass) with k, m = 4, 2
         bench.K, bench.M, bench.ERASED = 4, 2, [0, 1]
+        n = 1024
+        g = torch.Generator(device="cuda").manual_seed(0x1E0E)
+        objs = torch.randint(0, 256, (n, MiB), dtype=torch.uint8, device="cuda", generator=g)
+        bs, _ = le.layout("vandrs", (4, 2, 8), MiB)
+        parity = torch.empty((n, 2 * bs), dtype=torch.uint8, device="cuda")
+        le.device.encode("vandrs", (4, 2, 8), objs, MiB, parity)
+        torch.cuda.synchronize()
         t0 = time.time()
-        cpu = bench.cpu_baseline(MiB, args.cpu_seconds, threads)
+        cpu = bench.cpu_baseline(objs, parity, MiB, n, args.cpu_seconds)
         print(json.dumps({"config": "cfg0: vandrs RS(4,2,8) 1 MiB encode+decode, CPU port",
                           "cpu": cpu, "wall_s": round(time.time() - t0, 1)}), flush=True)
 
