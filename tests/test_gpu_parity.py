@@ -472,12 +472,12 @@ def test_file_helpers(gpu, le, tmp_path, monkeypatch):
 
 @pytest.mark.parametrize("w", [16, 32])
 @pytest.mark.parametrize("env", [
-    {},                                        # shipped: byte-plane v_perm, 2 columns per lane
-    {"LEOEC_GFP_CPT": "1"},                    # byte-plane, 1 column per lane
-    {"LEOEC_GFP_BPC": "1"},                    # byte-plane, 1 block per CU: long grid-stride walks
+    {},                                        # shipped: bitsliced planes (gfs_apply)
+    {"LEOEC_GFW_FORM": "0"},                   # byte-plane v_perm, 2 columns per lane
+    {"LEOEC_GFW_FORM": "0", "LEOEC_GFP_CPT": "1"},  # byte-plane, 1 column per lane
+    {"LEOEC_GFW_FORM": "0", "LEOEC_GFP_BPC": "1"},  # byte-plane, 1 block per CU: long walks
     {"LEOEC_GFW_FORM": "1"},                   # w=16: 2-bit-field v_perm; w=32: shift-and-add
     {"LEOEC_GFW_FORM": "2"},                   # shift-and-add
-    {"LEOEC_GFW_FORM": "3"},                   # bitsliced planes (gfs_apply)
 ])
 def test_gfw_kernel_forms_agree(gpu, le, oracle, w, env, measure):
     """w = 16 / 32 through every kernel form: encode vs the oracle, decode
