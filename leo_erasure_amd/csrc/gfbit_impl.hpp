@@ -8,6 +8,13 @@
 #include "knobs.hpp"
 
 namespace leoec {
+namespace detail {
+// cauchyrs(10,4,8) encode with its bitmatrix compiled in (cbm_inst.hip):
+// launches it and returns true when the plan's coefficients are that
+// matrix's and Knobs::gfbit_cbm selects it; *rc = the launch's status.
+bool launch_cbm(const GfBitApply& p, hipStream_t s, int* rc);
+}  // namespace detail
+
 namespace gfbit_detail {
 
 using namespace detail;

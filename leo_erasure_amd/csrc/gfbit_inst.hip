@@ -303,6 +303,10 @@ int launch(const GfBitApply& p, hipStream_t s) {
     if (((uintptr_t)sh.base & 15u) || (sh.stride & 15u)) return LEOEC_E_ARG;
   for (const Shard& sh : p.out)
     if (((uintptr_t)sh.base & 15u) || (sh.stride & 15u)) return LEOEC_E_ARG;
+  {
+    int rc = LEOEC_OK;
+    if (launch_cbm(p, s, &rc)) return rc;
+  }
   const uint64_t ps = p.block_size / (uint64_t)w;
   // the narrowest tile of any form (64 lanes x 8 bytes, LEOEC_GFBIT_WG=64)
   // bounds the grid: every form's tile count is at most this

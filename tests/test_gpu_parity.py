@@ -273,6 +273,9 @@ def test_device_roundtrip_bench_shape(gpu, le):
                                  {"LEOEC_GFBIT_LW": "4", "LEOEC_GFBIT_PF": "0"},
                                  {"LEOEC_GFBIT_FORM": "1", "LEOEC_GFBIT_WG": "128"},
                                  {"LEOEC_GFBIT_WAVES": "4"}, {"LEOEC_GFBIT_WAVES": "5"},
+                                 {"LEOEC_GFBIT_CBM": "1"}, {"LEOEC_GFBIT_CBM": "2"},
+                                 {"LEOEC_GFBIT_CBM": "3"}, {"LEOEC_GFBIT_CBM": "4"},
+                                 {"LEOEC_GFBIT_CBM": "5"},
                                  {"LEOEC_GFBIT_FORM": "2"}],  # gfbx_apply (LDS-shared, split rows)
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_cauchy_kernel_forms_agree(gpu, le, oracle, env, measure):
@@ -412,6 +415,31 @@ def test_xcd_object_map_batches(gpu, le, oracle, measure, cls, k, m, w):
     for o in (0, 7, 8, 12):
         r = oracle.encode(cls, k, m, w, host[o, :size].tobytes())
         assert outs[0][o, :m * bs].tobytes() == b"".join(r[k:]), f"object {o}"
+
+
+@pytest.mark.parametrize("form", ["1", "2", "3", "4", "5"])
+def test_cauchy_compiled_bitmatrix_batches(gpu, le, oracle, measure, form):
+    """cauchyrs(10,4,8) encode with its bitmatrix compiled in (cbm_inst.hip,
+    LEOEC_GFBIT_CBM): batches of whole and ragged 1 MiB objects (a short last
+    data block, odd packets starting mid line), 13 objects (not a multiple of
+    the XCD map's 8): parity identical to the bitsliced kernel's for every
+    object and to the oracle's for some."""
+    k, m, w = 10, 4, 8
+    for size in (1048576, 1048576 - 333, 77777):
+        n = 13
+        bs, _ = le.layout("cauchyrs", (k, m, w), size)
+        host, objs = _batch(gpu, n, size, max(k, m) * bs, 57 + size % 97)
+        outs = []
+        for env in ("0", form):
+            measure.setenv("LEOEC_GFBIT_CBM", env)
+            parity = gpu.full((n, max(k, m) * bs), 0x5A, dtype=gpu.uint8, device="cuda")
+            le.device.encode("cauchyrs", (k, m, w), objs, size, parity)
+            gpu.cuda.synchronize()
+            outs.append(parity.cpu().numpy())
+        assert np.array_equal(outs[0], outs[1]), size
+        for o in (0, 7, 12):
+            r = oracle.encode("cauchyrs", k, m, w, host[o, :size].tobytes())
+            assert outs[1][o, :m * bs].tobytes() == b"".join(r[k:]), (size, o)
 
 
 @pytest.mark.parametrize("tgroup", ["5", "128"])
