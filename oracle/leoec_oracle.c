@@ -980,17 +980,17 @@ typedef struct {
   uint8_t *objs, *par, *tail;
   pthread_barrier_t *start, *done;
   volatile int *stop;
-  int err;
+  int err, pinned;
 } pinned_worker;
 
 static void *pinned_main(void *arg) {
   pinned_worker *W = arg;
 #if defined(__linux__)
-  if (W->cpu >= 0) {
+  if (W->cpu >= 0) {  /* best effort: a refused pin leaves the worker unpinned */
     cpu_set_t set;
     CPU_ZERO(&set);
     CPU_SET(W->cpu, &set);
-    if (pthread_setaffinity_np(pthread_self(), sizeof(set), &set)) W->err = 1;
+    W->pinned = pthread_setaffinity_np(pthread_self(), sizeof(set), &set) == 0;
   }
 #endif
   const int n = W->enc.o1 - W->enc.o0;
