@@ -31,7 +31,8 @@ const Knobs* read_env() {
   k->bitmatrix = env_int("LEOEC_BITMATRIX", k->bitmatrix);
   if (const char* e = std::getenv("LEOEC_HOST_STAGING")) {
     const std::string_view v(e);
-    k->host_staging = v == "pageable" ? 1 : v == "gather" ? 2 : v == "pinned" ? 3 : 0;
+    k->host_staging = v == "pageable" ? 1 : v == "gather" ? 2 : v == "pinned" ? 3
+                      : v == "zerocopy" ? 4 : 0;
   }
   k->stage_chunk_kib = env_int("LEOEC_STAGE_CHUNK_KIB", k->stage_chunk_kib);
   k->host_batch = env_int("LEOEC_HOST_BATCH", k->host_batch);

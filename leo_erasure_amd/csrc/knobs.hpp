@@ -14,7 +14,8 @@ namespace leoec {
 struct Knobs {
   // engine.cpp
   int bitmatrix = 0;         // LEOEC_BITMATRIX=1: cauchyrs through the generic bitmatrix kernel
-  int host_staging = 0;      // LEOEC_HOST_STAGING: 0 auto, 1 pageable, 2 gather, 3 pinned ring
+  int host_staging = 0;      // LEOEC_HOST_STAGING: 0 auto, 1 pageable, 2 gather, 3 pinned ring,
+                             //   4 zero-copy (kernels on pinned, device-mapped host memory)
   int stage_chunk_kib = 256; // LEOEC_STAGE_CHUNK_KIB: pinned-ring chunk
   int host_batch = 1;        // LEOEC_HOST_BATCH=0: host calls take the per-thread path only
   int batch_window_us = 0;   // LEOEC_BATCH_WINDOW_US: hold an idle-GPU batch open this long

@@ -607,24 +607,27 @@ def test_concurrent_callers(gpu, le, oracle):
 
 @pytest.mark.parametrize("staging,chunk_kib", [("pinned", "16"), ("pinned", "256"),
                                                ("pinned", "8192"), ("pageable", "256"),
-                                               ("gather", "256"), ("auto", "256")])
+                                               ("gather", "256"), ("auto", "256"),
+                                               ("zerocopy", "256")])
 def test_host_staging_forms(gpu, le, oracle, staging, chunk_kib, measure):
     """Host entry points (the NIF path) under every staging form: the plain
     pageable copies, the default (auto: gather for several host buffers),
     the gather form (one pinned copy per direction,
     engine.cpp stage_h2d_segs / stage_d2h_sync) and the pinned-ring
     measurement form with chunks small enough to wrap the 8-slot ring many
-    times within one call, and one chunk per object.  Encode / decode / repair bit-exact with the
+    times within one call, and one chunk per object, and the zero-copy form
+    (kernels on a pinned, device-mapped buffer; spans above its 16 MiB cap
+    take the copy forms).  Encode / decode / repair bit-exact with the
     oracle, including ragged sizes and a 64 MiB + 5 object."""
     measure.setenv("LEOEC_HOST_STAGING", staging)
     measure.setenv("LEOEC_STAGE_CHUNK_KIB", chunk_kib)
     cases = [("vandrs", 10, 4, 8, 1048576), ("vandrs", 10, 4, 8, 300001),
              ("cauchyrs", 10, 4, 8, 1048576 + 77), ("isars", 4, 2, 8, 65536 + 7),
              ("liberation", 4, 2, 7, 777777), ("vandrs", 6, 3, 32, 123457)]
-    if chunk_kib == "16" or staging in ("gather", "auto"):
+    if chunk_kib == "16" or staging in ("gather", "auto", "zerocopy"):
         # gather: a span above its 16 MiB pinned cap takes the pageable copies
         cases.append(("vandrs", 10, 4, 8, (64 << 20) + 5))
-    if staging in ("gather", "auto"):  # spans either side of the cap, D2H span > H2D span
+    if staging in ("gather", "auto", "zerocopy"):  # spans either side of the 16 MiB cap, D2H > H2D
         cases += [("vandrs", 10, 4, 8, 16 << 20), ("vandrs", 4, 6, 8, 5000),
                   ("vandrs", 2, 8, 8, 3000000)]
     for cls, k, m, w, size in cases:
