@@ -499,11 +499,12 @@ const std::thread::id g_load_thread = Staging::load_thread();
 // calls run on the device the dispatcher picks, hostq.cpp)
 thread_local Staging tl_staging[kMaxDevices];
 
-// Default (auto): gather when a direction has several separate host buffers
+// Default (auto): zero-copy (below, zc_ready) for spans up to kGatherMax;
+// above it, gather when a direction has several separate host buffers
 // (decode / repair: k survivor binaries in, e rebuilt blocks out), pageable
 // for one contiguous buffer (encode), measured best on each
-// (profiles/r01_v14_e2e_gather.log).  "gather" / "pageable" / "pinned" force
-// one form.
+// (profiles/r01_v14_e2e_gather.log).  "gather" / "pageable" / "pinned" /
+// "zerocopy" force one form.
 enum class StageForm { kAuto, kPageable, kGather, kRing, kZeroCopy };
 
 StageForm stage_form() {
@@ -548,16 +549,21 @@ uint8_t* gather_buf(Staging* st, size_t bytes) {
   return st->hbuf;
 }
 
-// Zero-copy form (StageForm::kZeroCopy): the call's blocks are packed by
-// host memcpys into one pinned, device-mapped buffer per thread, and the
-// kernel reads its inputs and writes its outputs there, over PCIe — no DMA
-// copy, one launch and one stream sync per call (a lone 1 MiB encode:
-// 90 us against 106 us with pageable copies, tools/zerocopy_probe.py).
-// Returns false (use the copy forms) when the form is off or the buffer
-// cannot be had.
+// Zero-copy form (the default since round 3 for spans up to kGatherMax;
+// LEOEC_HOST_STAGING=zerocopy forces it, pageable / gather / pinned force a
+// copy form): the call's blocks are packed by host memcpys into one pinned,
+// device-mapped buffer per thread and device, and the kernel reads its
+// inputs and writes its outputs there, over PCIe — no DMA copy, one launch
+// and one stream sync per call.  A lone 1 MiB encode: 90 us against 106 us
+// with pageable copies (tools/zerocopy_probe.py); 1 / 4 / 8 encode callers
+// +20 / +18 / +5 %, decode +7 / −8 / +8 % (profiles/r03_v10_e2e_zerocopy.log).
+// Returns false (use the copy forms) when the form is off, the span is
+// larger than kGatherMax, or the buffer cannot be had.
 bool zc_ready(Staging* st, size_t bytes) {
   st->zc = false;
-  if (stage_form() != StageForm::kZeroCopy || bytes == 0 || bytes > kGatherMax) return false;
+  const StageForm f = stage_form();
+  if ((f != StageForm::kZeroCopy && f != StageForm::kAuto) || bytes == 0 || bytes > kGatherMax)
+    return false;
   if (st->zcap < bytes) {
     if (st->zh) {
       (void)hipStreamSynchronize(st->stream);
