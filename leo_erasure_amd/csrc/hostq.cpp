@@ -71,6 +71,8 @@ struct Slot {
   uint8_t* h_out = nullptr;
   uint8_t* d_in = nullptr;
   uint8_t* d_out = nullptr;
+  uint8_t* z_in = nullptr;   // device addresses of h_in / h_out (zero-copy batches)
+  uint8_t* z_out = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
   hipEvent_t ev_blk = nullptr;  // the same, created hipEventBlockingSync (Knobs::hostq_sync = 2)
@@ -116,8 +118,10 @@ hipError_t wait_event(hipEvent_t ev) {
 }
 
 int slot_alloc(Slot* s) {
-  if (hipHostMalloc((void**)&s->h_in, kSlotBytes, hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc((void**)&s->h_out, kSlotBytes, hipHostMallocDefault) != hipSuccess ||
+  if (hipHostMalloc((void**)&s->h_in, kSlotBytes, hipHostMallocMapped) != hipSuccess ||
+      hipHostMalloc((void**)&s->h_out, kSlotBytes, hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&s->z_in, s->h_in, 0) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&s->z_out, s->h_out, 0) != hipSuccess ||
       hipMalloc((void**)&s->d_in, kSlotBytes) != hipSuccess ||
       hipMalloc((void**)&s->d_out, kSlotBytes) != hipSuccess ||
       hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -157,11 +161,17 @@ bool same_map(const HostJob& a, const HostJob& b) {
 // fails every job (the copies, the event).
 int launch_slot(Slot* s) {
   Clock::time_point t = Clock::now();
-  int rc = hipMemcpyAsync(s->d_in, s->h_in, s->used_in, hipMemcpyHostToDevice, s->stream) ==
-                   hipSuccess
-               ? LEOEC_OK
-               : LEOEC_E_HIP;
-  if (rc == LEOEC_OK && hipEventRecord(s->ev_h2d, s->stream) != hipSuccess) rc = LEOEC_E_HIP;
+  // Knobs::hostq_zc (measurement): the kernels read the pinned input arena
+  // and write the pinned output arena over PCIe, no DMA copy either way
+  const bool zc = knobs().hostq_zc != 0;
+  uint8_t* din = zc ? s->z_in : s->d_in;
+  uint8_t* dout = zc ? s->z_out : s->d_out;
+  int rc = zc ? LEOEC_OK
+              : hipMemcpyAsync(s->d_in, s->h_in, s->used_in, hipMemcpyHostToDevice, s->stream) ==
+                        hipSuccess
+                    ? LEOEC_OK
+                    : LEOEC_E_HIP;
+  if (rc == LEOEC_OK && !zc && hipEventRecord(s->ev_h2d, s->stream) != hipSuccess) rc = LEOEC_E_HIP;
   stat_add(11, us_since(t));
   t = Clock::now();
   const size_t n = s->jobs.size();
@@ -175,9 +185,9 @@ int launch_slot(Slot* s) {
     const int k = J.plan->code->k, r = (int)J.plan->want.size();
     std::vector<Shard> in(k), out(r);
     for (int b = 0; b < k; ++b)
-      in[b] = Shard{s->d_in + s->in_off[i] + (uint64_t)b * J.in_blk, sin, J.in_valid[b]};
+      in[b] = Shard{din + s->in_off[i] + (uint64_t)b * J.in_blk, sin, J.in_valid[b]};
     for (int o = 0; o < r; ++o)
-      out[o] = Shard{s->d_out + s->out_off[i] + (uint64_t)o * J.out_blk, sout, J.out_valid};
+      out[o] = Shard{dout + s->out_off[i] + (uint64_t)o * J.out_blk, sout, J.out_valid};
     int run_rc;
 #ifdef LEOEC_MEASURE
     // fault injection (LEOEC_HOSTQ_FAIL_BS): this run's launch "fails"
@@ -193,7 +203,9 @@ int launch_slot(Slot* s) {
   }
   stat_add(12, us_since(t));
   t = Clock::now();
-  if (rc == LEOEC_OK &&
+  if (rc == LEOEC_OK && zc && hipEventRecord(s->ev_h2d, s->stream) != hipSuccess)
+    rc = LEOEC_E_HIP;  // (zero-copy: the inputs are consumed when the launches end)
+  if (rc == LEOEC_OK && !zc &&
       hipMemcpyAsync(s->h_out, s->d_out, s->used_out, hipMemcpyDeviceToHost, s->stream) !=
           hipSuccess)
     rc = LEOEC_E_HIP;

@@ -30,6 +30,8 @@ struct Knobs {
                              //   per-thread path gathers k buffers: it tops out sooner)
   int hostq_fail_bs = 0;     // LEOEC_HOSTQ_FAIL_BS: batched launches of this block size report
                              //   a HIP error (fault injection: per-job status)
+  int hostq_zc = 0;          // LEOEC_HOSTQ_ZC=1: batches without DMA copies (kernels on the
+                             //   pinned, device-mapped arenas)
   int hostq_lanes = 0;       // LEOEC_HOSTQ_LANES: dispatcher lanes (0: one per gfx950 device;
                              //   N: N lanes, lane i on device i % devices)
   // kernels.hip / kernels_impl.hpp

@@ -762,7 +762,7 @@ def _capi_roundtrip(le, c, t):
 
 
 @pytest.mark.parametrize("form", ["product", "always-batch", "per-thread", "lanes4",
-                                  "lanes4-always-batch", "fail-one"])
+                                  "lanes4-always-batch", "fail-one", "zc-batch"])
 def test_host_batching_mixed_callers(gpu, le, oracle, form, request):
     """Cross-call batching (hostq.cpp): 24 threads call the C ABI at once with
     mixed classes, widths, sizes (ragged, and 9 MiB objects above the batch
@@ -780,7 +780,7 @@ def test_host_batching_mixed_callers(gpu, le, oracle, form, request):
     fail_bs = None
     if form != "product":
         ms = request.getfixturevalue("measure")
-        if form in ("always-batch", "lanes4-always-batch", "fail-one"):
+        if form in ("always-batch", "lanes4-always-batch", "fail-one", "zc-batch"):
             ms.setenv("LEOEC_HOSTQ_DIRECT", "0")
             ms.setenv("LEOEC_HOSTQ_DIRECT_MAP", "0")
         if form == "per-thread":
@@ -788,6 +788,8 @@ def test_host_batching_mixed_callers(gpu, le, oracle, form, request):
         if form.startswith("lanes4"):
             ms.setenv("LEOEC_HOSTQ_LANES", "4")
             assert len(le._lib.host_lanes()) == 4
+        if form == "zc-batch":
+            ms.setenv("LEOEC_HOSTQ_ZC", "1")
         if form == "fail-one":
             fail_bs = 1296  # cauchyrs(4,2,3) on 5000 B: bs = ceil16(5000 / 12) * 3
             ms.setenv("LEOEC_HOSTQ_FAIL_BS", str(fail_bs))
@@ -829,7 +831,7 @@ def test_host_batching_mixed_callers(gpu, le, oracle, form, request):
         stats(buf)
         lane_jobs(lanes)
         batches, jobs, launches = buf[0], buf[1], buf[2]
-        if form in ("always-batch", "lanes4-always-batch"):
+        if form in ("always-batch", "lanes4-always-batch", "zc-batch"):
             # 24 x 8 x 3 calls, minus the 9 MiB ones (per-thread path)
             assert jobs >= 24 * 8 * 3 * 0.8 and batches < jobs and launches > batches, list(buf)
         elif form == "per-thread":
