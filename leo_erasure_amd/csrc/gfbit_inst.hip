@@ -123,6 +123,169 @@ int launch_gfbx_8(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }
 
+// gfba_apply (measurement form, LEOEC_GFBIT_FORM=3; no accumulation, <= 16
+// inputs, every input's valid length a multiple of 16): the shipped
+// arithmetic (8-byte lanes, 64 accumulator VGPRs) fed by line-aligned
+// loads.  At the reference's 1 MiB geometry ps = 13,120 B, so odd packets
+// start mid cache line and every 512-B wave load of one touches 5 lines
+// instead of 4 (tools/packet_ceiling.hip: the same access pattern on
+// 128-B-aligned packets reads 0.756 against 0.69-0.72).  Each wave owns a
+// 512-B column of every packet; per input block it copies, for each packet,
+// the 128-B lines covering its column (5 lines when the column starts mid
+// line, 4 otherwise) into its own LDS slot with 16-byte buffer-to-LDS loads
+// (no VGPRs held by the copy), then reads its 8 bytes per lane from the slot
+// at the column's phase.  Two slots per packet: block j+1's copy is in
+// flight while block j is computed.  Waves never share LDS: no barriers.
+constexpr uint32_t kGfbaCol = 512;           // bytes of a packet per wave (64 lanes x 8 B)
+constexpr uint32_t kGfbaSlot = kGfbaCol + 128;  // lines covering a column at any 16-B phase
+
+template <int W, int R, int WG, bool CEIL, int NB>
+__global__ void __launch_bounds__(WG) gfba_apply(const GfbArgs<R> a) {
+  static_assert(NB >= 2 && NB <= 6, "slots per packet");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[WG / 64][NB][W][kGfbaSlot];
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / 64u);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t bid = a.xmap ? xcd_obj_map(blockIdx.x, gridDim.x, a.tiles) : blockIdx.x;
+  const uint32_t obj = bid / a.tiles;
+  const uint32_t tile = bid - obj * a.tiles;
+  const uint32_t col0 = tile * (WG / 64u) * kGfbaCol + wv * kGfbaCol;
+  if (col0 >= a.ps) return;  // wave-uniform: no barriers below
+  const uint64_t o64 = obj;
+  const int K = a.K;
+  // start of the lines holding packet x's column, and the column's phase in them
+  auto phase = [&](const DevShard& d, int x) -> uint32_t {
+    const uint64_t at = (uint64_t)(uintptr_t)(d.base + o64 * d.stride) + (uint64_t)x * a.ps + col0;
+    return __builtin_amdgcn_readfirstlane((uint32_t)at & 127u);
+  };
+  // W copies per block (one per packet, lanes past the lines masked off)
+  auto issue = [&](int j, int b) {
+    const DevShard d = a.in[j];
+    const auto rs = shard_rsrc(d.base, d.stride, d.valid, o64, 16u);
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const uint32_t sh = phase(d, x);
+      const uint32_t nl = sh ? (kGfbaCol + 128u) / 16u : kGfbaCol / 16u;
+      // an offset below the shard's start wraps past its range and reads zeros
+      const uint32_t vo = (uint32_t)x * a.ps + col0 - sh + lane * 16u;
+      if (lane < nl)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)&lds[wv][b][x][0], 16, vo, 0, 0, 2);
+    }
+  };
+  LaneVec<2> acc[R][W];
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int x = 0; x < W; ++x) acc[i][x].v[0] = acc[i][x].v[1] = 0u;
+#pragma unroll
+  for (int u = 0; u < NB - 1; ++u)
+    if (u < K) issue(u, u);
+  int b = 0;
+  for (int j = 0; j < K; ++j) {
+    // block j's copies landed; the next min(NB-2, K-1-j) blocks' stay in flight
+    const int ahead = K - 1 - j < NB - 2 ? K - 1 - j : NB - 2;
+    if (NB == 2 || ahead == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W) : "memory");
+    else if (NB == 3 || ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * W) : "memory");
+    else if (NB == 4 || ahead == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * W) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * W) : "memory");
+    // the reads are inline asm: for a plain LDS read the compiler waits for
+    // every copy in flight (vmcnt(0)), draining the ring; their results are
+    // tied to the lgkmcnt wait below so nothing uses them earlier
+    static_assert(W == 8, "gfba_apply: eight packets per block");
+    uint64_t t[W];
+    const DevShard d = a.in[j];
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const uint32_t sh = phase(d, x);
+      const auto lp = (__attribute__((address_space(3))) const uint8_t*)&lds[wv][b][x][sh + lane * 8u];
+      asm volatile("ds_read_b64 %0, %1" : "=v"(t[x]) : "v"((uint32_t)(size_t)lp));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]),
+                   "+v"(t[6]), "+v"(t[7]));
+    LaneVec<2> y[W];
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      y[x].v[0] = (uint32_t)t[x];
+      y[x].v[1] = (uint32_t)(t[x] >> 32);
+    }
+    // the slot block j-1 used is free (its reads were consumed last iteration)
+    if (j + NB - 1 < K) issue(j + NB - 1, b == 0 ? NB - 1 : b - 1);
+    b = b + 1 == NB ? 0 : b + 1;
+    uint32_t c[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) c[i] = a.coef[i][j];
+    gfb_accumulate<W, R, 2, CEIL>(acc, y, c);
+  }
+  const uint32_t off = col0 + lane * 8u;
+  if (off >= a.ps) return;  // (ps is a multiple of 16: off < ps => all 8 bytes in the packet)
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    uint8_t* p = const_cast<uint8_t*>(a.out[i].base) + o64 * a.out[i].stride;
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const uint32_t pk = (uint32_t)x * a.ps;
+      lv_store<2>(p + pk, off, packet_valid(a.out[i].valid, x, a.ps), acc[i][x]);
+    }
+  }
+}
+
+// gfba_apply applies: w = 8, no accumulation, every input's valid length a
+// multiple of 16 (the copy's range check then zero-fills exactly the bytes
+// past it).
+bool gfba_applies(const GfBitApply& p, int w, bool acc, int nk) {
+  if (w != 8 || acc || nk > kMaxK) return false;
+  for (const Shard& sh : p.in)
+    if (sh.valid % 16u) return false;
+  return true;
+}
+
+template <int R, int WG, bool CEIL, int NB>
+int launch_gfba_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
+                  hipStream_t s) {
+  GfbArgs<R> a;
+  a.K = nk;
+  a.ps = (uint32_t)(p.block_size / 8u);
+  a.tiles = (a.ps + (WG / 64u) * kGfbaCol - 1u) / ((WG / 64u) * kGfbaCol);
+  for (int j = 0; j < kMaxK; ++j)
+    a.in[j] = j < nk ? dev_shard(p.in[j0 + j], o0) : DevShard{nullptr, 0, 0, 0};
+  for (int i = 0; i < R; ++i) {
+    a.out[i] = dev_shard(p.out[r0 + i], o0);
+    for (int j = 0; j < kMaxK; ++j)
+      a.coef[i][j] = j < nk ? p.coef[(size_t)(r0 + i) * p.K + j0 + j] : 0u;
+  }
+  a.xmap = (a.tiles <= kObjMapMaxTiles && knobs().gfbit_xmap != 0) ? 1u : 0u;
+  hipLaunchKernelGGL((gfba_apply<8, R, WG, CEIL, NB>), dim3((uint32_t)(no * a.tiles)), dim3(WG),
+                     0, s, a);
+  return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
+}
+
+template <int WG, bool CEIL, int NB>
+GfbFn pick_gfba(int r) {
+  static const GfbFn tbl[kMaxR] = {&launch_gfba_t<1, WG, CEIL, NB>, &launch_gfba_t<2, WG, CEIL, NB>,
+                                   &launch_gfba_t<3, WG, CEIL, NB>, &launch_gfba_t<4, WG, CEIL, NB>};
+  return tbl[r - 1];
+}
+
+GfbFn pick_gfba_knobs(int r) {
+  const Knobs& kn = knobs();
+  // LEOEC_GFBIT_PF = blocks in flight (1..3: 2..4 slots per packet);
+  // LEOEC_GFBIT_WG=256: four waves per workgroup (each its own slots);
+  // LEOEC_GFBIT_CEIL=1: XOR-only memory form (not a code)
+  const int pf = kn.gfbit_pf;
+  if (kn.gfbit_wg == 256) {
+    if (kn.gfbit_ceil) return pick_gfba<256, true, 2>(r);
+    return pick_gfba<256, false, 2>(r);
+  }
+  if (kn.gfbit_ceil) return pf >= 3 ? pick_gfba<64, true, 4>(r) : pf == 2 ? pick_gfba<64, true, 3>(r) : pick_gfba<64, true, 2>(r);
+  if (pf >= 5) return pick_gfba<64, false, 6>(r);
+  if (pf == 4) return pick_gfba<64, false, 5>(r);
+  if (pf == 3) return pick_gfba<64, false, 4>(r);
+  if (pf == 2) return pick_gfba<64, false, 3>(r);
+  return pick_gfba<64, false, 2>(r);
+}
+
 template <int W, int R, bool ACC>
 int launch_gfb_lds_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
                      hipStream_t s) {
@@ -250,8 +413,9 @@ GfbFn pick2(int w, int r, bool acc) {
 }
 #endif  // LEOEC_MEASURE
 
-GfbFn pick(int w, int r, bool acc, int nk) {
+GfbFn pick(const GfBitApply& p, int w, int r, bool acc, int nk) {
   (void)nk;
+  (void)p;
 #ifdef LEOEC_MEASURE
   // LEOEC_GFBIT_FORM=1: gfb2_apply (LEOEC_GFBIT_LW=1: 4 bytes per lane per
   // packet at w = 8; LEOEC_GFBIT_PF=1: its prefetching loop)
@@ -259,6 +423,7 @@ GfbFn pick(int w, int r, bool acc, int nk) {
   // chunk, no accumulation), the shipped kernel otherwise
   if (knobs().gfbit_form == 2 && w == 8 && r == 4 && !acc && nk <= kMaxK)
     return &launch_gfbx_8;
+  if (knobs().gfbit_form == 3 && gfba_applies(p, w, acc, nk)) return pick_gfba_knobs(r);
   if (knobs().gfbit_form == 1) {
     // LEOEC_GFBIT_WG=128: 16-byte lanes in 128-lane workgroups, next block in flight
     if (w == 8 && knobs().gfbit_wg == 128) return pick_r2<8, 4, 1, 128>(r, acc);
@@ -318,7 +483,7 @@ int launch(const GfBitApply& p, hipStream_t s) {
       const int nr = (p.R - r0 < kMaxR) ? p.R - r0 : kMaxR;
       for (int j0 = 0; j0 < p.K; j0 += kMaxK) {
         const int nk = (p.K - j0 < kMaxK) ? p.K - j0 : kMaxK;
-        const int rc = pick(w, nr, j0 > 0, nk)(p, r0, j0, nk, o0, no, s);
+        const int rc = pick(p, w, nr, j0 > 0, nk)(p, r0, j0, nk, o0, no, s);
         if (rc) return rc;
       }
     }

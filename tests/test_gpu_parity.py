@@ -442,6 +442,46 @@ def test_cauchy_compiled_bitmatrix_batches(gpu, le, oracle, measure, form):
             assert outs[1][o, :m * bs].tobytes() == b"".join(r[k:]), (size, o)
 
 
+@pytest.mark.parametrize("env", [{}, {"LEOEC_GFBIT_WG": "256"}, {"LEOEC_GFBIT_PF": "2"},
+                                 {"LEOEC_GFBIT_PF": "3"}, {"LEOEC_GFBIT_PF": "4"}, {"LEOEC_GFBIT_PF": "5"}],
+                         ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()) or "default")
+def test_cauchy_aligned_copy_batches(gpu, le, oracle, measure, env):
+    """cauchyrs through gfba_apply (LEOEC_GFBIT_FORM=3: line-aligned 16-byte
+    copies into per-wave LDS slots, read back at each packet's phase): object
+    rows at every 16-byte phase mod 128 (row stride = k*bs + 48), sizes whose
+    blocks are full, short (last block 103,936 of 104,960 B), one packet of
+    16 B, and empty (size 1,040: block 9 holds nothing); encode parity equal
+    to the shipped kernel's and to the oracle's, decode and repair of
+    erased data and parity blocks in place."""
+    measure.setenv("LEOEC_GFBIT_FORM", "3")
+    for key, v in env.items():
+        measure.setenv(key, v)
+    for k, m, size in [(10, 4, 1048576), (10, 4, 1048576 - 16 * 21), (10, 4, 77776),
+                       (10, 4, 1040), (6, 3, 300000), (4, 2, 262144 + 4096)]:
+        w, n = 8, 11
+        bs, _ = le.layout("cauchyrs", (k, m, w), size)
+        stride = max(k, m) * bs + 48
+        host, objs = _batch(gpu, n, size, stride, 91 + size % 89)
+        ref = objs.clone()
+        outs = []
+        for form in ("0", "3"):
+            measure.setenv("LEOEC_GFBIT_FORM", form)
+            parity = gpu.full((n, m * bs + 48), 0x5A, dtype=gpu.uint8, device="cuda")
+            le.device.encode("cauchyrs", (k, m, w), objs, size, parity)
+            gpu.cuda.synchronize()
+            outs.append(parity.cpu().numpy())
+        assert np.array_equal(outs[0], outs[1]), (k, m, size)
+        for o in (0, 5, n - 1):
+            r = oracle.encode("cauchyrs", k, m, w, host[o, :size].tobytes())
+            assert outs[1][o, :m * bs].tobytes() == b"".join(r[k:]), (k, m, size, o)
+        er = list(range(min(m, k)))
+        objs[:, :len(er) * bs] = 0
+        le.device.decode("cauchyrs", (k, m, w), objs, size,
+                         gpu.from_numpy(outs[1]).cuda(), er)
+        gpu.cuda.synchronize()
+        assert gpu.equal(objs, ref), (k, m, size)
+
+
 @pytest.mark.parametrize("tgroup", ["5", "128"])
 def test_gf8_segment_map_forms(gpu, le, oracle, measure, tgroup):
     """gf8 tile map 4 (XCD-interleaved runs of consecutive tiles, shipped for
