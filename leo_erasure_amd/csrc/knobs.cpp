@@ -70,6 +70,7 @@ const Knobs* read_env() {
   k->gfbit_form = env_int("LEOEC_GFBIT_FORM", k->gfbit_form);
   k->gfbit_waves = env_int("LEOEC_GFBIT_WAVES", k->gfbit_waves);
   k->gfbit_cbm = env_int("LEOEC_GFBIT_CBM", k->gfbit_cbm);
+  k->gfbit_edge = env_int("LEOEC_GFBIT_EDGE", k->gfbit_edge);
   return k;
 }
 
