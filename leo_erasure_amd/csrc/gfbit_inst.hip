@@ -349,25 +349,8 @@ GfbFn pick_r_waves(int r, bool acc) {
   return tbl[acc ? 1 : 0][r - 1];
 }
 
-// Edge waves loading with the default cache policy (LEOEC_GFBIT_EDGE=1|2).
-template <int EDGE>
-GfbFn pick_r_edge(int r, bool acc) {
-  static const GfbFn tbl[2][kMaxR] = {
-      {&launch_gfb_t<8, 1, 2, false, kPF, false, 0, kThreads, 0, 0, EDGE>,
-       &launch_gfb_t<8, 2, 2, false, kPF, false, 0, kThreads, 0, 0, EDGE>,
-       &launch_gfb_t<8, 3, 2, false, kPF, false, 0, kThreads, 0, 0, EDGE>,
-       &launch_gfb_t<8, 4, 2, false, kPF, false, 0, kThreads, 0, 0, EDGE>},
-      {&launch_gfb_t<8, 1, 2, true, kPF, false, 0, kThreads, 0, 0, EDGE>,
-       &launch_gfb_t<8, 2, 2, true, kPF, false, 0, kThreads, 0, 0, EDGE>,
-       &launch_gfb_t<8, 3, 2, true, kPF, false, 0, kThreads, 0, 0, EDGE>,
-       &launch_gfb_t<8, 4, 2, true, kPF, false, 0, kThreads, 0, 0, EDGE>}};
-  return tbl[acc ? 1 : 0][r - 1];
-}
-
 GfbFn pick_measure8(int r, bool acc) {
   const Knobs& kn = knobs();
-  if (kn.gfbit_edge == 1) return pick_r_edge<1>(r, acc);
-  if (kn.gfbit_edge == 2) return pick_r_edge<2>(r, acc);
   // LEOEC_GFBIT_WAVES=4|5: the shipped form under a register cap
   if (kn.gfbit_waves == 4) return pick_r_waves<8, 2, kPF, 4>(r, acc);
   if (kn.gfbit_waves == 5) return pick_r_waves<8, 2, kPF, 5>(r, acc);

@@ -862,9 +862,7 @@ struct LaneVec {
   uint32_t v[LW];
 };
 
-// POL 0: non-temporal loads (streamed once); 1: default policy (the line
-// stays in L2 for a neighbouring tile that shares it).
-template <int LW, int POL = 0>
+template <int LW>
 __device__ __forceinline__ LaneVec<LW> lv_load(const uint8_t* p, uint32_t off, uint32_t valid) {
   LaneVec<LW> r;
   if (LW == 4) {
@@ -876,13 +874,11 @@ __device__ __forceinline__ LaneVec<LW> lv_load(const uint8_t* p, uint32_t off, u
     const uint32_t bytes = 4u * LW;
     if (off + bytes <= valid) {
       if (LW == 2) {
-        const vt x = POL ? *reinterpret_cast<const vt*>(p + off)
-                         : __builtin_nontemporal_load(reinterpret_cast<const vt*>(p + off));
+        const vt x = __builtin_nontemporal_load(reinterpret_cast<const vt*>(p + off));
         r.v[0] = x[0];
         r.v[LW - 1] = x[LW == 2 ? 1 : 0];
       } else {
-        r.v[0] = POL ? *reinterpret_cast<const uint32_t*>(p + off)
-                     : __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p + off));
+        r.v[0] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p + off));
       }
     } else {
 #pragma unroll
@@ -922,18 +918,11 @@ __device__ __forceinline__ void lv_store(uint8_t* p, uint32_t off, uint32_t vali
   }
 }
 
-// plain: packets (bit x) loaded with the default cache policy instead of
-// non-temporal (wave-uniform; 0 in the shipped form)
 template <int W, int LW>
 __device__ __forceinline__ void gfb_load_block(const uint8_t* base, uint32_t ps, uint32_t off,
-                                               uint32_t bv, LaneVec<LW> (&y)[W], uint32_t plain = 0u) {
+                                               uint32_t bv, LaneVec<LW> (&y)[W]) {
 #pragma unroll
-  for (int x = 0; x < W; ++x) {
-    if ((plain >> x) & 1u)
-      y[x] = lv_load<LW, 1>(base + (uint32_t)x * ps, off, packet_valid(bv, x, ps));
-    else
-      y[x] = lv_load<LW, 0>(base + (uint32_t)x * ps, off, packet_valid(bv, x, ps));
-  }
+  for (int x = 0; x < W; ++x) y[x] = lv_load<LW>(base + (uint32_t)x * ps, off, packet_valid(bv, x, ps));
 }
 
 // acc[i] ^= c[i] * y for every output i (y is consumed: it is doubled in
@@ -983,12 +972,8 @@ __device__ __forceinline__ void gfb_accumulate(LaneVec<LW> (&acc)[R][W], LaneVec
 //   PFD = 0: load block j, then compute on it.
 //   WAVES > 0: ask the register allocator for at least WAVES waves per SIMD
 //            (amdgpu_waves_per_eu; 4 caps the kernel at 128 VGPRs).
-//   EDGE (measurement): the edge waves of a tile (first, last, and every wave
-//            of a packet's last tile) load with the default cache policy:
-//            1 every packet, 2 the packets that start mid line (the lines a
-//            neighbouring tile shares stay in L2 for it).
 template <int W, int R, int LW, bool ACC, int PFD = 1, bool CEIL = false, int KR = 0,
-          int WG = kThreads, int XMAP = 0, int WAVES = 0, int EDGE = 0>
+          int WG = kThreads, int XMAP = 0, int WAVES = 0>
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(WAVES > 0 ? WAVES : 1, 8)))
 gfbit_apply(const GfbArgs<R> a) {
   constexpr uint32_t LB = 4u * LW;
@@ -1018,23 +1003,8 @@ gfbit_apply(const GfbArgs<R> a) {
 #pragma unroll
     for (int i = 0; i < R; ++i) c[i] = a.coef[i][j];
   };
-  bool edge = false;
-  if constexpr (EDGE != 0) {
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / 64u);
-    edge = wv == 0u || wv == WG / 64u - 1u || tile + 1u == a.tiles;
-  }
   auto load = [&](int j, LaneVec<LW> (&y)[W]) {
-    const uint8_t* base = a.in[j].base + o64 * a.in[j].stride;
-    uint32_t plain = 0u;
-    if constexpr (EDGE == 1) plain = edge ? 0xFFFFFFFFu : 0u;
-    if constexpr (EDGE == 2) {
-      if (edge) {
-        const uint32_t b0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)base);
-#pragma unroll
-        for (int x = 0; x < W; ++x) plain |= ((b0 + (uint32_t)x * a.ps) & 127u) ? 1u << x : 0u;
-      }
-    }
-    gfb_load_block<W, LW>(base, a.ps, off, a.in[j].valid, y, plain);
+    gfb_load_block<W, LW>(a.in[j].base + o64 * a.in[j].stride, a.ps, off, a.in[j].valid, y);
   };
   if constexpr (KR > 0) {
     LaneVec<LW> ys[KR][W];

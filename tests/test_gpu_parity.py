@@ -276,8 +276,7 @@ def test_device_roundtrip_bench_shape(gpu, le):
                                  {"LEOEC_GFBIT_CBM": "1"}, {"LEOEC_GFBIT_CBM": "2"},
                                  {"LEOEC_GFBIT_CBM": "3"}, {"LEOEC_GFBIT_CBM": "4"},
                                  {"LEOEC_GFBIT_CBM": "5"},
-                                 {"LEOEC_GFBIT_FORM": "2"},  # gfbx_apply (LDS-shared, split rows)
-                                 {"LEOEC_GFBIT_EDGE": "1"}, {"LEOEC_GFBIT_EDGE": "2"}],
+                                 {"LEOEC_GFBIT_FORM": "2"}],  # gfbx_apply (LDS-shared, split rows)
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_cauchy_kernel_forms_agree(gpu, le, oracle, env, measure):
     """cauchyrs through the generic masked-bitmatrix kernel and through every
@@ -547,7 +546,6 @@ def test_file_helpers(gpu, le, tmp_path, monkeypatch):
     {"LEOEC_GFW_FORM": "0", "LEOEC_GFP_BPC": "1"},  # byte-plane, 1 block per CU: long walks
     {"LEOEC_GFW_FORM": "1"},                   # w=16: 2-bit-field v_perm; w=32: shift-and-add
     {"LEOEC_GFW_FORM": "2"},                   # shift-and-add
-    {"LEOEC_GFS_PF": "2"},                     # gfs_apply, two inputs in flight
 ])
 def test_gfw_kernel_forms_agree(gpu, le, oracle, w, env, measure):
     """w = 16 / 32 through every kernel form: encode vs the oracle, decode
