@@ -77,6 +77,8 @@ def parse(argv=None):
     p.add_argument("--cpu-objects", type=int, default=1024,
                    help="objects in the cpu_baseline sample (copied from rank 0's batch)")
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    p.add_argument("--no-ceiling", action="store_true",
+                   help="skip the live access-pattern ceiling of the headline kernel")
     p.add_argument("--traffic", default=",".join(
         os.path.join(ROOT, "profiles", f) for f in ("pmc_traffic.json", "pmc_traffic_64MiB.json")),
                    help="PMC-derived HBM bytes per launch, comma-separated files; the one whose "
@@ -131,6 +133,62 @@ class GpuBackend:
 
     def event(self):
         return self.torch.cuda.Event(enable_timing=True)
+
+    def pattern_ceiling(self, objs, size, parity, enc_bytes, rounds=5, reps=20):
+        """SURVEY §8(d)'s achievable-copy figure for the headline kernel, live:
+        the shipped encode (product library) and the same launch with the GF
+        product replaced by XOR (every data column into every parity column:
+        the same loads and stores, no tables; measurement library,
+        LEOEC_GF8_VARIANT=7, gf8_exp.hip — not a code) timed in alternating
+        rounds on this batch.  Overwrites `parity`.  Median per-launch times."""
+        import os
+        import statistics
+        lib = self.le._lib
+        if not os.path.exists(lib.MEASURE_LIB_PATH):
+            return {"achieved": None, "error": "measurement build absent (make -C leo_erasure_amd/csrc measure)"}
+        prod = lib.library_path()
+        key = "LEOEC_GF8_VARIANT"
+        old_env = os.environ.get(key)
+        times = {"shipped": [], "ceiling": []}
+        try:
+            for _ in range(rounds):
+                for which in ("shipped", "ceiling"):
+                    if which == "ceiling":
+                        lib.use_library(lib.MEASURE_LIB_PATH)
+                        os.environ[key] = "7"
+                        lib.measure_reload()
+                        if self.le.gf_init() != "ok":
+                            raise RuntimeError("gf_init failed in the measurement library")
+                    else:
+                        lib.use_library(prod)
+                    for _ in range(3):
+                        self.encode(objs, size, parity)
+                    ev = [self.event() for _ in range(reps + 1)]
+                    self.sync()
+                    ev[0].record()
+                    for i in range(reps):
+                        self.encode(objs, size, parity)
+                        ev[i + 1].record()
+                    self.sync()
+                    times[which] += [ev[i].elapsed_time(ev[i + 1]) for i in range(reps)]
+        finally:
+            if old_env is None:
+                os.environ.pop(key, None)
+            else:
+                os.environ[key] = old_env
+            if lib.library_path() != prod:
+                lib.measure_reload()
+            lib.use_library(prod)
+        ship_ms = statistics.median(times["shipped"])
+        ceil_ms = statistics.median(times["ceiling"])
+        ship = enc_bytes / (ship_ms * 1e-3) / 1e9
+        ceil = enc_bytes / (ceil_ms * 1e-3) / 1e9
+        return {"kernel": "gf8_apply<10,4> COPY form: same loads and stores, XOR for the GF "
+                          "product (measurement library, LEOEC_GF8_VARIANT=7; not a code)",
+                "achieved": round(ceil, 1), "frac": round(ceil / HBM_PEAK_GBS, 4),
+                "shipped_achieved": round(ship, 1),
+                "shipped_over_ceiling": round(ship / ceil, 4),
+                "sample": f"{rounds} alternating rounds x {reps} launches each, medians"}
 
 
 # ---------------------------------------------------------------------------
@@ -517,6 +575,13 @@ def run_rank(args, be, rank, world, dist=None):
         rec["cpu_baseline"] = cb
         if "parity_vs_gpu" in cb:
             verified = verified and cb["parity_vs_gpu"]["equal"]
+    if world == 1 and not args.no_ceiling and hasattr(be, "pattern_ceiling"):
+        # after the CPU leg: this overwrites parity
+        try:
+            rec["roofline"]["pattern_ceiling"] = be.pattern_ceiling(objs, size, parity, enc_bytes)
+        except Exception as e:  # never discard the measurement over the ceiling leg
+            rec["roofline"]["pattern_ceiling"] = {"achieved": None,
+                                                  "error": f"{type(e).__name__}: {e}"}
     rec["verified"] = verified
     return rec, verified
 
