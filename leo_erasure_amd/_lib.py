@@ -84,6 +84,11 @@ def _load(path=LIB_PATH):
     if hasattr(L, "leoec_measure_reload"):
         L.leoec_measure_reload.argtypes = []
         L.leoec_measure_reload.restype = None
+    if hasattr(L, "leoec_measure_xor_pattern_dev"):  # measurement build (xor_pattern.hip)
+        L.leoec_measure_xor_pattern_dev.argtypes = [
+            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+            ctypes.c_uint64, ctypes.c_void_p]
+        L.leoec_measure_xor_pattern_dev.restype = ctypes.c_int
     _loaded[path] = L
     return L
 

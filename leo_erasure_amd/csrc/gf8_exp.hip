@@ -51,6 +51,8 @@ ChunkFn gf8_variant_part<LEOEC_GF8_EXP_PART>(int v) {
     case 27: return &launch_gf8_t<10, 4, false, 1, true, 1, true, false, false, 5, 64>;   // copy wg64
     case 31: return &launch_gf8_t<10, 4, false, 1, true, 1, true, false, false, 5, 256, 2, true>;  // copy buffer
     case 35: return &launch_gf8_t<10, 4, false, 1, true, 0, false, false, true, 5, 64, 0, true>;  // buffer ld/st wg64, run-time tile map
+    case 39: return &launch_gf8_t<10, 4, false, 1, true, 0, true, false, true>;   // copy, shipped shape
+    case 43: return &launch_gf8_t<10, 4, false, 1, true, 0, true, false, true, 5, 64>;   // copy, shipped shape, wg64
 #endif
     default: return nullptr;
   }
