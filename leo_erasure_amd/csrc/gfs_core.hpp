@@ -208,7 +208,10 @@ LEOEC_GFS_HD P32Step p32_step(const uint32_t (&pl)[16]) {
   return n;
 }
 
-template <int R, int T>
+// ALLB (measurement only, not a code): every pair of every coefficient taken
+// as "both bits set", with no tests — the same VALU work as the coefficient
+// 0xFFFFFFFF without the scalar tests and branches.
+template <int R, int T, bool ALLB = false>
 LEOEC_GFS_HD void mac_p32_pair(uint32_t (&pl)[16], uint32_t (&acc)[R][16], const PairMasks (&c)[R],
                                uint32_t any) {
   const P32Step n = p32_step<T>(pl);
@@ -224,6 +227,11 @@ LEOEC_GFS_HD void mac_p32_pair(uint32_t (&pl)[16], uint32_t (&acc)[R][16], const
   q1[6] = n.r6;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
+    if constexpr (ALLB) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[r][i] = xor3(acc[r][i], q0[i], q1[i]);
+      continue;
+    }
     // wave-uniform: scalar branches
     if ((c[r].both >> T) & 1u) {
 #pragma unroll
@@ -238,8 +246,13 @@ LEOEC_GFS_HD void mac_p32_pair(uint32_t (&pl)[16], uint32_t (&acc)[R][16], const
       for (int i = 0; i < 16; ++i) acc[r][i] ^= q1[i];
     }
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+  // ALLB: keep the scheduler from hoisting work across pairs (without the
+  // shipped form's branches it raised the kernel to 128 VGPRs and spilled)
+  if constexpr (ALLB) __builtin_amdgcn_sched_barrier(0);
+#endif
   if constexpr (T + 2 < 32) {
-    if ((any >> (T + 2)) == 0u) return;  // no coefficient has a higher bit
+    if (!ALLB && (any >> (T + 2)) == 0u) return;  // no coefficient has a higher bit
     // commit P_{T+1} (logical register i of P_{T+1} lives in pl[(i - T - 1) mod 16])
     pl[(15 - T) & 15] = n.r0;
     pl[(0 - T) & 15] = n.r1;
@@ -250,13 +263,13 @@ LEOEC_GFS_HD void mac_p32_pair(uint32_t (&pl)[16], uint32_t (&acc)[R][16], const
     pl[(15 - T) & 15] = n2.r1;
     pl[(0 - T) & 15] = n2.r2;
     pl[(4 - T) & 15] = n2.r6;
-    mac_p32_pair<R, T + 2>(pl, acc, c, any);
+    mac_p32_pair<R, T + 2, ALLB>(pl, acc, c, any);
   }
 }
 
 // acc[r] ^= c[r] * x over GF(2^32), 16 words per lane in the packed layout
 // (transpose<16> of the 16 words; pl destroyed).
-template <int R>
+template <int R, bool ALLB = false>
 LEOEC_GFS_HD void mac_p32(uint32_t (&pl)[16], uint32_t (&acc)[R][16], const uint32_t (&c)[R]) {
   PairMasks m[R];
   uint32_t any = 0u;
@@ -265,7 +278,7 @@ LEOEC_GFS_HD void mac_p32(uint32_t (&pl)[16], uint32_t (&acc)[R][16], const uint
     m[r] = pair_masks(c[r]);
     any |= c[r];
   }
-  mac_p32_pair<R, 0>(pl, acc, m, any);
+  mac_p32_pair<R, 0, ALLB>(pl, acc, m, any);
 }
 
 }  // namespace gfs

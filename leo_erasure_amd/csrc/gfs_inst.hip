@@ -15,6 +15,7 @@
 // ran ~15 % slower.
 #include "gfs_core.hpp"
 #include "kernels_impl.hpp"
+#include "knobs.hpp"
 
 namespace leoec {
 namespace detail {
@@ -69,20 +70,28 @@ __device__ __forceinline__ void gfs_tail(uint32_t t0, uint32_t valid, uint32_t (
   }
 }
 
-// Input j (raw words in pl) into the R accumulators.
-template <int W, int R>
+// Input j (raw words in pl) into the R accumulators.  MODE (measurement
+// builds only; not a code): 1 every coefficient forced to 0xFFFFFFFF at run
+// time (an opaque scalar the compiler cannot fold: the shipped tests and
+// branches run, all taken), 2 the same VALU work with no tests compiled in
+// (gfs_core.hpp ALLB).
+template <int W, int R, int MODE = 0>
 __device__ __forceinline__ void gfs_step(const InCol& col, uint32_t t0, bool full,
                                          uint32_t (&pl)[kGfsRegs], uint32_t (&acc)[R][kGfsRegs]) {
   if (!full) gfs_tail(t0, col.valid, pl);
   gfs::transpose<kGfsRegs>(pl);
   uint32_t c[R];
+  uint32_t force = 0u;
+  if constexpr (MODE == 1) asm volatile("s_mov_b32 %0, -1" : "=s"(force));  // opaque: tests stay
 #pragma unroll
-  for (int r = 0; r < R; ++r) c[r] = col.coef[r];
-  if constexpr (W == 32) gfs::mac_p32<R>(pl, acc, c);
+  for (int r = 0; r < R; ++r) c[r] = col.coef[r] | force;
+  if constexpr (W == 32) gfs::mac_p32<R, MODE == 2>(pl, acc, c);
   else gfs::mac<16, R>(pl, acc, c);
 }
 
-template <int W, int R, bool ACC>
+// PF (measurement builds): inputs whose loads are in flight while one is
+// computed (1 shipped: two input buffers; 2: three).
+template <int W, int R, bool ACC, int MODE = 0, int PF = 1>
 __global__ void __launch_bounds__(kGfsLanes) __attribute__((amdgpu_waves_per_eu(4)))
 gfs_apply(const GfsArgs<R> a) {
   constexpr int NL = kGfsLoads;
@@ -107,20 +116,46 @@ gfs_apply(const GfsArgs<R> a) {
   // two input buffers: input j+1 is loaded into one while input j is
   // transposed and accumulated in place in the other
   const int K = a.K;
+  if constexpr (PF == 2) {
+    // three input buffers: inputs j+1 and j+2 in flight while j is computed
+    uint32_t b0[kGfsRegs], b1[kGfsRegs], b2[kGfsRegs];
+    auto col = [&](int i) { return a.col[i < K ? i : K]; };
+    InCol c0 = col(0), c1 = col(1), c2 = col(2);
+    gfs_load(gfs_rsrc(c0.base, c0.stride, c0.valid, o), t0, b0);
+    gfs_load(gfs_rsrc(c1.base, c1.stride, c1.valid, o), t0, b1);
+    for (int j = 0;; j += 3) {
+      gfs_load(gfs_rsrc(c2.base, c2.stride, c2.valid, o), t0, b2);
+      const InCol c3 = col(j + 3);
+      gfs_step<W, R, MODE>(c0, t0, full, b0, acc);
+      if (j + 1 >= K) break;
+      gfs_load(gfs_rsrc(c3.base, c3.stride, c3.valid, o), t0, b0);
+      const InCol c4 = col(j + 4);
+      gfs_step<W, R, MODE>(c1, t0, full, b1, acc);
+      if (j + 2 >= K) break;
+      gfs_load(gfs_rsrc(c4.base, c4.stride, c4.valid, o), t0, b1);
+      const InCol c5 = col(j + 5);
+      gfs_step<W, R, MODE>(c2, t0, full, b2, acc);
+      if (j + 3 >= K) break;
+      c0 = c3;
+      c1 = c4;
+      c2 = c5;
+    }
+  } else {
   uint32_t bufa[kGfsRegs], bufb[kGfsRegs];
   InCol cur = a.col[0], nx = a.col[K > 1 ? 1 : K];
   gfs_load(gfs_rsrc(cur.base, cur.stride, cur.valid, o), t0, bufa);
   for (int j = 0;; j += 2) {
     gfs_load(gfs_rsrc(nx.base, nx.stride, nx.valid, o), t0, bufb);  // input j+1 (or empty)
     const InCol nx2 = a.col[j + 2 < K ? j + 2 : K];
-    gfs_step<W, R>(cur, t0, full, bufa, acc);
+    gfs_step<W, R, MODE>(cur, t0, full, bufa, acc);
     if (j + 1 >= K) break;
     gfs_load(gfs_rsrc(nx2.base, nx2.stride, nx2.valid, o), t0, bufa);  // input j+2 (or empty)
     const InCol nx3 = a.col[j + 3 < K ? j + 3 : K];
-    gfs_step<W, R>(nx, t0, full, bufb, acc);
+    gfs_step<W, R, MODE>(nx, t0, full, bufb, acc);
     if (j + 2 >= K) break;
     cur = nx2;
     nx = nx3;
+  }
   }
   // A column of zeros and ones (encode's column 0) skips the bit domain: it
   // is XORed into the accumulators after these are transposed back to
@@ -152,7 +187,7 @@ gfs_apply(const GfsArgs<R> a) {
   }
 }
 
-template <int W, int R, bool ACC>
+template <int W, int R, bool ACC, int MODE = 0, int PF = 1>
 int launch_gfs_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   GfsArgs<R> a;
   uint32_t vmin = 0xFFFFFFFFu;
@@ -198,7 +233,7 @@ int launch_gfs_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   a.xmap = a.tiles <= kObjMapMaxTiles ? 1u : 0u;
   const uint64_t grid = c.no * a.tiles;
   if (grid == 0 || grid > 0x7FFFFFFFull) return LEOEC_E_ARG;
-  hipLaunchKernelGGL((gfs_apply<W, R, ACC>), dim3((uint32_t)grid), dim3(kGfsLanes), 0, s, a);
+  hipLaunchKernelGGL((gfs_apply<W, R, ACC, MODE, PF>), dim3((uint32_t)grid), dim3(kGfsLanes), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }
 
@@ -213,6 +248,15 @@ ChunkFn gfs_pick_w(int r, bool acc) {
 }
 
 ChunkFn gfs_pick(int w, int r, bool acc) {
+#ifdef LEOEC_MEASURE
+  // LEOEC_GFS_MODE=1|2 (w = 32, 4 rows, one input chunk; timing only, wrong bytes)
+  const int mode = knobs().gfs_mode;
+  if (w == 32 && r == 4 && !acc && mode == 1) return &launch_gfs_t<32, 4, false, 1>;
+  if (w == 32 && r == 4 && !acc && mode == 2) return &launch_gfs_t<32, 4, false, 2>;
+  // LEOEC_GFS_PF=2: two inputs in flight (4 rows, one input chunk)
+  if (r == 4 && !acc && knobs().gfs_pf == 2)
+    return w == 16 ? &launch_gfs_t<16, 4, false, 0, 2> : &launch_gfs_t<32, 4, false, 0, 2>;
+#endif
   return w == 16 ? gfs_pick_w<16>(r, acc) : gfs_pick_w<32>(r, acc);
 }
 
