@@ -822,12 +822,10 @@ typedef struct {
 /* One object of a bench job: RSCoding::doEncode's stripe staging, then the
  * encode, or the in-place decode of the job's erased data blocks.  `tail` is
  * a k*bs scratch buffer. */
-static void bench_object(const bench_job *J, int o, uint8_t *tail) {
+static void bench_object_at(const bench_job *J, const uint8_t *obj, uint8_t *par, uint8_t *tail) {
   uint64_t bs = J->bs;
   int k = J->k, m = J->m;
   {
-    const uint8_t *obj = J->objs + (uint64_t)o * J->stride;
-    uint8_t *par = J->parity + (uint64_t)o * m * bs;
     /* stripe staging exactly as RSCoding::doEncode: whole blocks alias the
      * object, the tail block is copied into a zeroed buffer */
     const uint8_t *blk[256];
@@ -868,6 +866,11 @@ static void bench_object(const bench_job *J, int o, uint8_t *tail) {
         }
       }
   }
+}
+
+static void bench_object(const bench_job *J, int o, uint8_t *tail) {
+  bench_object_at(J, J->objs + (uint64_t)o * J->stride,
+                  J->parity + (uint64_t)o * J->m * J->bs, tail);
 }
 
 static void *bench_worker(void *arg) {
@@ -972,6 +975,20 @@ int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride
  * object payload (2 x objects x size per round) of pass i; returns the number
  * of passes (<= max_passes) or a negative ORC_E_*.  parity_out (nobj x m x
  * bs) receives the workers' encode of the sample, for the parity check. */
+/* Objects are handed out from a shared counter per phase (chunks of
+ * kBenchChunk), not as fixed slices: a worker whose core another tenant of
+ * the host takes for a while does fewer objects instead of holding every
+ * other worker at the round's barrier. */
+enum { kBenchChunk = 2 };
+
+typedef struct {
+  const uint8_t **obj;  /* per object of the sample: its first-touched copy */
+  uint8_t **par;        /* and its parity rows */
+  int nobj;
+  volatile int next[2]; /* per phase (0 encode, 1 decode): next object to hand out */
+  pthread_barrier_t mid; /* workers only: every encode done before any decode */
+} bench_queue;
+
 typedef struct {
   const uint8_t *src;
   uint64_t src_stride;
@@ -980,8 +997,20 @@ typedef struct {
   uint8_t *objs, *par, *tail;
   pthread_barrier_t *start, *done;
   volatile int *stop;
+  bench_queue *q;
+  int o0;               /* first object of this worker's first-touched slice */
   int err, pinned;
 } pinned_worker;
+
+static void bench_phase(const bench_job *J, bench_queue *q, int ph, uint8_t *tail) {
+  for (;;) {
+    const int o = __atomic_fetch_add(&q->next[ph], kBenchChunk, __ATOMIC_RELAXED);
+    if (o >= q->nobj) return;
+    const int e = o + kBenchChunk < q->nobj ? o + kBenchChunk : q->nobj;
+    for (int i = o; i < e; i++)
+      if (q->obj[i]) bench_object_at(J, q->obj[i], q->par[i], tail);  /* NULL: its worker failed */
+  }
+}
 
 static void *pinned_main(void *arg) {
   pinned_worker *W = arg;
@@ -1011,13 +1040,19 @@ static void *pinned_main(void *arg) {
   W->enc.parity = W->dec.parity = W->par;
   W->enc.o1 = W->dec.o1 = n;
   W->enc.o0 = W->dec.o0 = 0;
+  if (!W->err)
+    for (int o = 0; o < n; o++) {
+      W->q->obj[W->o0 + o] = W->objs + (uint64_t)o * size;
+      W->q->par[W->o0 + o] = W->par + (uint64_t)o * m * bs;
+    }
   for (;;) {
     pthread_barrier_wait(W->start);
     if (*W->stop) break;
-    if (!W->err)
-      for (int o = 0; o < n; o++) bench_object(&W->enc, o, W->tail);
-    if (!W->err)
-      for (int o = 0; o < n; o++) bench_object(&W->dec, o, W->tail);
+    /* (a failed allocation anywhere stops the run: the main thread checks
+     * every worker's err before the first timed round) */
+    bench_phase(&W->enc, W->q, 0, W->tail);
+    pthread_barrier_wait(&W->q->mid);
+    bench_phase(&W->dec, W->q, 1, W->tail);
     pthread_barrier_wait(W->done);
   }
   return NULL;
@@ -1047,12 +1082,19 @@ int orc_bench_rs8_pinned(int k, int m, const uint8_t *src, uint64_t src_stride, 
   pthread_barrier_init(&start, NULL, (unsigned)threads + 1);
   pthread_barrier_init(&done, NULL, (unsigned)threads + 1);
   volatile int stop = 0;
+  bench_queue Q;
+  Q.obj = calloc((size_t)nobj, sizeof(*Q.obj));
+  Q.par = calloc((size_t)nobj, sizeof(*Q.par));
+  Q.nobj = nobj;
+  Q.next[0] = Q.next[1] = 0;
+  pthread_barrier_init(&Q.mid, NULL, (unsigned)threads);
   pinned_worker *Ws = calloc((size_t)threads, sizeof(pinned_worker));
   pthread_t *th = calloc((size_t)threads, sizeof(pthread_t));
   for (int t = 0; t < threads; t++) {
     pinned_worker *W = &Ws[t];
     W->src = src; W->src_stride = src_stride; W->cpu = cpus ? cpus[t] : -1;
-    W->start = &start; W->done = &done; W->stop = &stop;
+    W->start = &start; W->done = &done; W->stop = &stop; W->q = &Q;
+    W->o0 = (int)((long long)nobj * t / threads);
     bench_job *E = &W->enc, *D = &W->dec;
     E->op = 0; E->k = k; E->m = m; E->nout = PE.nout; E->simd = simd; E->size = size; E->bs = bs;
     E->o0 = (int)((long long)nobj * t / threads);
@@ -1063,15 +1105,19 @@ int orc_bench_rs8_pinned(int k, int m, const uint8_t *src, uint64_t src_stride, 
     D->surv = PD.surv;
     pthread_create(&th[t], NULL, pinned_main, W);
   }
-  /* round 0 (untimed): the first touch is done and the caches are warm */
+  /* round 0 (untimed): the first touch is done and the caches are warm.
+   * The main thread resets the queue's counters between rounds, while every
+   * worker waits at `start`. */
+  int np = 0, any_err = 0;
   pthread_barrier_wait(&start);
   pthread_barrier_wait(&done);
-  int np = 0;
+  for (int t = 0; t < threads; t++) any_err |= Ws[t].err;
   double t_all = 0.0;
-  while (np < max_passes && (t_all < total_s || np < min_passes)) {
+  while (!any_err && np < max_passes && (t_all < total_s || np < min_passes)) {
     double t0 = now_s(), dt;
     int reps = 0;
     do {
+      Q.next[0] = Q.next[1] = 0;
       pthread_barrier_wait(&start);
       pthread_barrier_wait(&done);
       reps++;
@@ -1094,6 +1140,8 @@ int orc_bench_rs8_pinned(int k, int m, const uint8_t *src, uint64_t src_stride, 
     free(W->objs); free(W->par); free(W->tail);
   }
   free(Ws); free(th);
+  free((void *)Q.obj); free(Q.par);
+  pthread_barrier_destroy(&Q.mid);
   pthread_barrier_destroy(&start);
   pthread_barrier_destroy(&done);
   bench_plan_free(&PE);

@@ -71,3 +71,20 @@ def test_pinned_baseline_parity(oracle):
     oracle.bench_rs8(0, 10, 4, objs, size, size, n, ref, threads=2)
     assert len(rates) >= 3 and all(r > 0 for r in rates)
     assert np.array_equal(par, ref)
+
+
+def test_pinned_baseline_queue_ragged(oracle):
+    """The baseline's shared object queue (chunks of 2): an odd object count,
+    more workers than chunks; several rounds of encode + in-place decode keep
+    the objects intact, so the last round's parity still equals the oracle's."""
+    n, size = 5, 70001
+    objs = np.random.default_rng(11).integers(0, 256, (n, size), dtype=np.uint8)
+    bs = oracle.block_size(10, 8, size)
+    par = np.zeros((n, 4 * bs), np.uint8)
+    ref = np.zeros_like(par)
+    cpus, _ = bench.pick_cpus(4)
+    rates = oracle.bench_rs8_pinned(10, 4, objs, size, [0, 1, 2, 3], 4, cpus, 0.02, 0.1,
+                                    parity_out=par)
+    oracle.bench_rs8(0, 10, 4, objs, size, size, n, ref, threads=1)
+    assert len(rates) >= 3 and all(r > 0 for r in rates)
+    assert np.array_equal(par, ref)
