@@ -241,6 +241,10 @@ GfbFn pick_r2(int r, bool acc) {
 // gfb2_apply's launch table of width W (gfbit_w.hip).
 template <int W>
 GfbFn measure2(int r, bool acc);
+
+// The measurement form the LEOEC_GFBIT_* knobs select for this launch
+// (gfbit_measure.hip), or nullptr for the shipped form.
+GfbFn pick_measure(const GfBitApply& p, int w, int r, bool acc, int nk);
 #endif  // LEOEC_MEASURE
 
 }  // namespace gfbit_detail
