@@ -187,156 +187,6 @@ gfs_apply(const GfsArgs<R> a) {
   }
 }
 
-#ifdef LEOEC_MEASURE
-// ---------------------------------------------------------------------------
-// Measurement only (LEOEC_GFS_MODE=3): vandrs(10,4,32) encode with its
-// coefficient matrix compiled in — what per-launch code (a kernel generated
-// for one matrix) would buy over the shipped kernel's run-time bit tests.
-// The 9 bitsliced columns of the encode matrix (column 0, all ones, goes
-// through the word domain as in the shipped kernel), rows 0..3; the launcher
-// takes this kernel only when the plan's coefficients equal the table.
-struct Rs10x4w32 {
-  static constexpr int K = 9;
-  static constexpr uint32_t c[9][4] = {
-      {0x00000001u, 0xe21aaaa9u, 0x8b34e9d1u, 0xd5600003u},
-      {0x00000001u, 0x5e924924u, 0x249b6db7u, 0xaa800002u},
-      {0x00000001u, 0x6fe40000u, 0x99bffffdu, 0x7fe00000u},
-      {0x00000001u, 0xf0cccccfu, 0x7fe00000u, 0x55400000u},
-      {0x00000001u, 0x9b4b6db4u, 0x6dadb6dbu, 0x80200002u},
-      {0x00000001u, 0x8b34e9d1u, 0xaa800002u, 0xffc00003u},
-      {0x00000001u, 0xf9a7fffcu, 0x68cb972eu, 0x2aa00001u},
-      {0x00000001u, 0x667fffffu, 0xffc00002u, 0xaa800003u},
-      {0x00000001u, 0x3ff00001u, 0x55400001u, 0x7fe00001u}};
-};
-
-// acc ^= the pair-(T, T+1) part of coefficient CV times x (q0 = x*a^T,
-// q1 = x*a^(T+1)), decided at compile time
-// (inline asm: with every coefficient bit known, plain XORs let the
-// optimiser reassociate the whole accumulation across pairs and outputs,
-// which kept dozens of partial sums live and spilled hundreds of VGPRs)
-template <uint32_t CV, int T>
-__device__ __forceinline__ void spec_acc(uint32_t (&acc)[16], const uint32_t (&q0)[16],
-                                         const uint32_t (&q1)[16]) {
-  constexpr uint32_t b0 = (CV >> T) & 1u, b1 = (CV >> (T + 1)) & 1u;
-  if constexpr (b0 && b1) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-      asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(acc[i]) : "v"(q0[i]), "v"(q1[i]));
-  } else if constexpr (b0) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) asm("v_xor_b32 %0, %0, %1" : "+v"(acc[i]) : "v"(q0[i]));
-  } else if constexpr (b1) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) asm("v_xor_b32 %0, %0, %1" : "+v"(acc[i]) : "v"(q1[i]));
-  }
-}
-
-template <class C, int J, int T>
-__device__ __forceinline__ void spec_pair(uint32_t (&pl)[16], uint32_t (&acc)[4][16]) {
-  const gfs::P32Step n = gfs::p32_step<T>(pl);
-  uint32_t q0[16], q1[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    q0[i] = pl[(i - T) & 15];
-    q1[i] = pl[(i - 1 - T) & 15];
-  }
-  q1[0] = n.r0;
-  q1[1] = n.r1;
-  q1[2] = n.r2;
-  q1[6] = n.r6;
-  spec_acc<C::c[J][0], T>(acc[0], q0, q1);
-  spec_acc<C::c[J][1], T>(acc[1], q0, q1);
-  spec_acc<C::c[J][2], T>(acc[2], q0, q1);
-  spec_acc<C::c[J][3], T>(acc[3], q0, q1);
-  constexpr uint32_t any = C::c[J][0] | C::c[J][1] | C::c[J][2] | C::c[J][3];
-  if constexpr (T + 2 < 32 && (any >> (T + 2)) != 0u) {
-    pl[(15 - T) & 15] = n.r0;
-    pl[(0 - T) & 15] = n.r1;
-    pl[(1 - T) & 15] = n.r2;
-    pl[(5 - T) & 15] = n.r6;
-    const gfs::P32Step n2 = gfs::p32_step<T + 1>(pl);
-    pl[(14 - T) & 15] = n2.r0;
-    pl[(15 - T) & 15] = n2.r1;
-    pl[(0 - T) & 15] = n2.r2;
-    pl[(4 - T) & 15] = n2.r6;
-    spec_pair<C, J, T + 2>(pl, acc);
-  }
-}
-
-// input j (planes in pl) into the accumulators: one compile-time body per
-// input, picked by a uniform switch (the input loop itself stays a run-time
-// loop as in gfs_apply: unrolled over the inputs, the straight-line kernel
-// spilled ~950 VGPRs)
-template <class C, int J>
-__device__ __forceinline__ void spec_case(int j, uint32_t (&pl)[kGfsRegs], uint32_t (&acc)[4][kGfsRegs]) {
-  if (j == J) {
-    spec_pair<C, J, 0>(pl, acc);
-    return;
-  }
-  if constexpr (J + 1 < C::K) spec_case<C, J + 1>(j, pl, acc);
-}
-
-template <class C>
-__global__ void __launch_bounds__(kGfsLanes) __attribute__((amdgpu_waves_per_eu(1)))
-gfs_spec(const GfsArgs<4> a) {
-  constexpr int NL = kGfsLoads;
-  constexpr uint32_t TB = kGfsTile;
-  const uint32_t b = a.xmap ? xcd_obj_map(blockIdx.x, gridDim.x, a.tiles) : blockIdx.x;
-  const uint32_t obj = b / a.tiles;
-  const uint32_t t0 = (b - obj * a.tiles) * TB;
-  const bool full = t0 + TB <= a.vmin;
-  const uint64_t o = obj;
-  uint32_t acc[4][kGfsRegs];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int k = 0; k < kGfsRegs; ++k) acc[r][k] = 0u;
-  const int K = C::K;
-  uint32_t bufa[kGfsRegs], bufb[kGfsRegs];
-  InCol cur = a.col[0], nx = a.col[1];
-  gfs_load(gfs_rsrc(cur.base, cur.stride, cur.valid, o), t0, bufa);
-  for (int j = 0;; j += 2) {
-    gfs_load(gfs_rsrc(nx.base, nx.stride, nx.valid, o), t0, bufb);  // input j+1 (or empty)
-    const InCol nx2 = a.col[j + 2 < K ? j + 2 : K];
-    if (!full) gfs_tail(t0, cur.valid, bufa);
-    gfs::transpose<kGfsRegs>(bufa);
-    spec_case<C, 0>(j, bufa, acc);
-    if (j + 1 >= K) break;
-    gfs_load(gfs_rsrc(nx2.base, nx2.stride, nx2.valid, o), t0, bufa);  // input j+2 (or empty)
-    const InCol nx3 = a.col[j + 3 < K ? j + 3 : K];
-    if (!full) gfs_tail(t0, nx.valid, bufb);
-    gfs::transpose<kGfsRegs>(bufb);
-    spec_case<C, 0>(j + 1, bufb, acc);
-    if (j + 2 >= K) break;
-    cur = nx2;
-    nx = nx3;
-  }
-  const InCol oc = a.ones;
-  uint32_t bufc[kGfsRegs];
-  gfs_load(gfs_rsrc(oc.base, oc.stride, oc.valid, o), t0, bufc);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) gfs::transpose<kGfsRegs>(acc[r]);
-  if (!full) gfs_tail(t0, oc.valid, bufc);
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-    if (oc.coef[r] & 1u) {
-#pragma unroll
-      for (int i = 0; i < kGfsRegs; ++i) acc[r][i] ^= bufc[i];
-    }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    uint8_t* p = const_cast<uint8_t*>(a.out[r].base) + o * a.out[r].stride;
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const uint32_t off = t0 + (uint32_t)i * (kGfsLanes * 16u) + threadIdx.x * 16u;
-      const u32x4 v = {acc[r][4 * i], acc[r][4 * i + 1], acc[r][4 * i + 2], acc[r][4 * i + 3]};
-      if (full) st16<true>(p + off, v);
-      else store_guarded(p, off, a.out[r].valid, v);
-    }
-  }
-}
-#endif  // LEOEC_MEASURE
-
 template <int W, int R, bool ACC, int MODE = 0, int PF = 1>
 int launch_gfs_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   GfsArgs<R> a;
@@ -383,18 +233,7 @@ int launch_gfs_t(const GfApply& p, const Chunk& c, hipStream_t s) {
   a.xmap = a.tiles <= kObjMapMaxTiles ? 1u : 0u;
   const uint64_t grid = c.no * a.tiles;
   if (grid == 0 || grid > 0x7FFFFFFFull) return LEOEC_E_ARG;
-#ifdef LEOEC_MEASURE
-  if constexpr (MODE == 3 && W == 32 && R == 4 && !ACC) {
-    bool match = a.K == Rs10x4w32::K && ones >= 0;
-    for (int j = 0; match && j < a.K; ++j)
-      for (int r = 0; r < 4; ++r) match = match && a.col[j].coef[r] == Rs10x4w32::c[j][r];
-    if (match) {
-      hipLaunchKernelGGL((gfs_spec<Rs10x4w32>), dim3((uint32_t)grid), dim3(kGfsLanes), 0, s, a);
-      return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
-    }
-  }
-#endif
-  hipLaunchKernelGGL((gfs_apply<W, R, ACC, MODE == 3 ? 0 : MODE, PF>), dim3((uint32_t)grid), dim3(kGfsLanes), 0, s, a);
+  hipLaunchKernelGGL((gfs_apply<W, R, ACC, MODE, PF>), dim3((uint32_t)grid), dim3(kGfsLanes), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }
 
@@ -414,8 +253,6 @@ ChunkFn gfs_pick(int w, int r, bool acc) {
   const int mode = knobs().gfs_mode;
   if (w == 32 && r == 4 && !acc && mode == 1) return &launch_gfs_t<32, 4, false, 1>;
   if (w == 32 && r == 4 && !acc && mode == 2) return &launch_gfs_t<32, 4, false, 2>;
-  // LEOEC_GFS_MODE=3: vandrs(10,4,32) encode with its matrix compiled in (a code)
-  if (w == 32 && r == 4 && !acc && mode == 3) return &launch_gfs_t<32, 4, false, 3>;
   // LEOEC_GFS_PF=2: two inputs in flight (4 rows, one input chunk)
   if (r == 4 && !acc && knobs().gfs_pf == 2)
     return w == 16 ? &launch_gfs_t<16, 4, false, 0, 2> : &launch_gfs_t<32, 4, false, 0, 2>;

@@ -547,7 +547,6 @@ def test_file_helpers(gpu, le, tmp_path, monkeypatch):
     {"LEOEC_GFW_FORM": "1"},                   # w=16: 2-bit-field v_perm; w=32: shift-and-add
     {"LEOEC_GFW_FORM": "2"},                   # shift-and-add
     {"LEOEC_GFS_PF": "2"},                     # gfs_apply, two inputs in flight
-    {"LEOEC_GFS_MODE": "3"},                   # vandrs(10,4,32) encode, matrix compiled in
 ])
 def test_gfw_kernel_forms_agree(gpu, le, oracle, w, env, measure):
     """w = 16 / 32 through every kernel form: encode vs the oracle, decode
