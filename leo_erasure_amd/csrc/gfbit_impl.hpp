@@ -23,7 +23,7 @@ using GfbFn = int (*)(const GfBitApply&, int r0, int j0, int nk, uint64_t o0, ui
                       hipStream_t);
 
 template <int W, int R, int LW, bool ACC, int PF, bool CEIL = false, int KR = 0,
-          int WG = kThreads, int XMAP = 0, int WAVES = 0, bool FAST = false>
+          int WG = kThreads, int XMAP = 0, int WAVES = 0>
 int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
                  hipStream_t s) {
   GfbArgs<R> a;
@@ -41,7 +41,7 @@ int launch_gfb_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint6
   // kObjMapMaxTiles tiles; Knobs::gfbit_xmap = 0 turns it off (A/B)
   a.xmap = (XMAP == 0 && a.tiles <= kObjMapMaxTiles && knobs().gfbit_xmap != 0) ? 1u : 0u;
   if (KR > 0 && nk > KR) return LEOEC_E_ARG;
-  hipLaunchKernelGGL((gfbit_apply<W, R, LW, ACC, PF, CEIL, KR, WG, XMAP, WAVES, FAST>),
+  hipLaunchKernelGGL((gfbit_apply<W, R, LW, ACC, PF, CEIL, KR, WG, XMAP, WAVES>),
                      dim3((uint32_t)(no * a.tiles)), dim3(WG), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }

@@ -351,25 +351,8 @@ GfbFn pick_r_waves(int r, bool acc) {
   return tbl[acc ? 1 : 0][r - 1];
 }
 
-// Uniform full-tile fast path (LEOEC_GFBIT_FAST=1): unguarded loads and
-// stores in every tile inside all shards' valid bytes.
-template <int W, int LW>
-GfbFn pick_r_fast(int r, bool acc) {
-  static const GfbFn tbl[2][kMaxR] = {
-      {&launch_gfb_t<W, 1, LW, false, kPF, false, 0, kThreads, 0, 0, true>,
-       &launch_gfb_t<W, 2, LW, false, kPF, false, 0, kThreads, 0, 0, true>,
-       &launch_gfb_t<W, 3, LW, false, kPF, false, 0, kThreads, 0, 0, true>,
-       &launch_gfb_t<W, 4, LW, false, kPF, false, 0, kThreads, 0, 0, true>},
-      {&launch_gfb_t<W, 1, LW, true, kPF, false, 0, kThreads, 0, 0, true>,
-       &launch_gfb_t<W, 2, LW, true, kPF, false, 0, kThreads, 0, 0, true>,
-       &launch_gfb_t<W, 3, LW, true, kPF, false, 0, kThreads, 0, 0, true>,
-       &launch_gfb_t<W, 4, LW, true, kPF, false, 0, kThreads, 0, 0, true>}};
-  return tbl[acc ? 1 : 0][r - 1];
-}
-
 GfbFn pick_measure8(int r, bool acc) {
   const Knobs& kn = knobs();
-  if (kn.gfbit_fast == 1) return pick_r_fast<8, 2>(r, acc);
   // LEOEC_GFBIT_WAVES=4|5: the shipped form under a register cap
   if (kn.gfbit_waves == 4) return pick_r_waves<8, 2, kPF, 4>(r, acc);
   if (kn.gfbit_waves == 5) return pick_r_waves<8, 2, kPF, 5>(r, acc);

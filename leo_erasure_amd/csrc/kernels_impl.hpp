@@ -918,44 +918,11 @@ __device__ __forceinline__ void lv_store(uint8_t* p, uint32_t off, uint32_t vali
   }
 }
 
-// Unguarded forms (the caller knows every byte is inside the shard).
-template <int LW>
-__device__ __forceinline__ LaneVec<LW> lv_load_full(const uint8_t* p) {
-  LaneVec<LW> r;
-  if constexpr (LW == 4) {
-    const u32x4 x = ld16<true>(p);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) r.v[e] = x[e];
-  } else if constexpr (LW == 2) {
-    typedef uint32_t v2 __attribute__((ext_vector_type(2)));
-    const v2 x = __builtin_nontemporal_load(reinterpret_cast<const v2*>(p));
-    r.v[0] = x[0];
-    r.v[1] = x[1];
-  } else {
-    r.v[0] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
-  }
-  return r;
-}
-
-template <int LW>
-__device__ __forceinline__ void lv_store_full(uint8_t* p, const LaneVec<LW>& x) {
-  if constexpr (LW == 4) {
-    st16<true>(p, u32x4{x.v[0], x.v[1], x.v[2], x.v[3]});
-  } else if constexpr (LW == 2) {
-    typedef uint32_t v2 __attribute__((ext_vector_type(2)));
-    __builtin_nontemporal_store(v2{x.v[0], x.v[1]}, reinterpret_cast<v2*>(p));
-  } else {
-    __builtin_nontemporal_store(x.v[0], reinterpret_cast<uint32_t*>(p));
-  }
-}
-
-template <int W, int LW, bool FULL = false>
+template <int W, int LW>
 __device__ __forceinline__ void gfb_load_block(const uint8_t* base, uint32_t ps, uint32_t off,
                                                uint32_t bv, LaneVec<LW> (&y)[W]) {
 #pragma unroll
-  for (int x = 0; x < W; ++x)
-    y[x] = FULL ? lv_load_full<LW>(base + (uint32_t)x * ps + off)
-                : lv_load<LW>(base + (uint32_t)x * ps, off, packet_valid(bv, x, ps));
+  for (int x = 0; x < W; ++x) y[x] = lv_load<LW>(base + (uint32_t)x * ps, off, packet_valid(bv, x, ps));
 }
 
 // acc[i] ^= c[i] * y for every output i (y is consumed: it is doubled in
@@ -1005,12 +972,18 @@ __device__ __forceinline__ void gfb_accumulate(LaneVec<LW> (&acc)[R][W], LaneVec
 //   PFD = 0: load block j, then compute on it.
 //   WAVES > 0: ask the register allocator for at least WAVES waves per SIMD
 //            (amdgpu_waves_per_eu; 4 caps the kernel at 128 VGPRs).
-//   FAST (measurement): tiles that lie inside every packet's valid bytes of
-//            every shard (all but the last tile of a packet, for whole
-//            blocks) run a copy of the body with plain loads and stores: no
-//            per-lane guards, so no branch merges in the loop.
-template <int W, int R, int LW, bool ACC, int PFD, bool CEIL, int KR, bool FULL>
-__device__ __forceinline__ void gfbit_body(const GfbArgs<R>& a, uint32_t obj, uint32_t off) {
+template <int W, int R, int LW, bool ACC, int PFD = 1, bool CEIL = false, int KR = 0,
+          int WG = kThreads, int XMAP = 0, int WAVES = 0>
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(WAVES > 0 ? WAVES : 1, 8)))
+gfbit_apply(const GfbArgs<R> a) {
+  constexpr uint32_t LB = 4u * LW;
+  const uint32_t bid = XMAP == 1 ? xcd_group(blockIdx.x, gridDim.x)
+                       : (XMAP == 2 || a.xmap) ? xcd_obj_map(blockIdx.x, gridDim.x, a.tiles)
+                                               : blockIdx.x;
+  const uint32_t obj = bid / a.tiles;
+  const uint32_t tile = bid - obj * a.tiles;
+  const uint32_t off = packet_lane_off(tile, threadIdx.x, WG, LB);
+  if (off >= a.ps) return;
   const uint64_t o64 = obj;
   LaneVec<LW> acc[R][W];
 #pragma unroll
@@ -1019,9 +992,8 @@ __device__ __forceinline__ void gfbit_body(const GfbArgs<R>& a, uint32_t obj, ui
     for (int x = 0; x < W; ++x) {
       if (ACC) {
         const uint32_t pk = (uint32_t)x * a.ps;
-        acc[i][x] = FULL ? lv_load_full<LW>(a.out[i].base + o64 * a.out[i].stride + pk + off)
-                         : lv_load<LW>(a.out[i].base + o64 * a.out[i].stride + pk, off,
-                                       packet_valid(a.out[i].valid, x, a.ps));
+        acc[i][x] = lv_load<LW>(a.out[i].base + o64 * a.out[i].stride + pk, off,
+                                packet_valid(a.out[i].valid, x, a.ps));
       } else {
 #pragma unroll
         for (int e = 0; e < LW; ++e) acc[i][x].v[e] = 0u;
@@ -1032,7 +1004,7 @@ __device__ __forceinline__ void gfbit_body(const GfbArgs<R>& a, uint32_t obj, ui
     for (int i = 0; i < R; ++i) c[i] = a.coef[i][j];
   };
   auto load = [&](int j, LaneVec<LW> (&y)[W]) {
-    gfb_load_block<W, LW, FULL>(a.in[j].base + o64 * a.in[j].stride, a.ps, off, a.in[j].valid, y);
+    gfb_load_block<W, LW>(a.in[j].base + o64 * a.in[j].stride, a.ps, off, a.in[j].valid, y);
   };
   if constexpr (KR > 0) {
     LaneVec<LW> ys[KR][W];
@@ -1072,37 +1044,9 @@ __device__ __forceinline__ void gfbit_body(const GfbArgs<R>& a, uint32_t obj, ui
 #pragma unroll
     for (int x = 0; x < W; ++x) {
       const uint32_t pk = (uint32_t)x * a.ps;
-      if (FULL) lv_store_full<LW>(p + pk + off, acc[i][x]);
-      else lv_store<LW>(p + pk, off, packet_valid(a.out[i].valid, x, a.ps), acc[i][x]);
+      lv_store<LW>(p + pk, off, packet_valid(a.out[i].valid, x, a.ps), acc[i][x]);
     }
   }
-}
-
-template <int W, int R, int LW, bool ACC, int PFD = 1, bool CEIL = false, int KR = 0,
-          int WG = kThreads, int XMAP = 0, int WAVES = 0, bool FAST = false>
-__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(WAVES > 0 ? WAVES : 1, 8)))
-gfbit_apply(const GfbArgs<R> a) {
-  constexpr uint32_t LB = 4u * LW;
-  const uint32_t bid = XMAP == 1 ? xcd_group(blockIdx.x, gridDim.x)
-                       : (XMAP == 2 || a.xmap) ? xcd_obj_map(blockIdx.x, gridDim.x, a.tiles)
-                                               : blockIdx.x;
-  const uint32_t obj = bid / a.tiles;
-  const uint32_t tile = bid - obj * a.tiles;
-  const uint32_t off = packet_lane_off(tile, threadIdx.x, WG, LB);
-  if (off >= a.ps) return;
-  if constexpr (FAST) {
-    // wave-uniform: the tile's last byte of the last packet is inside every shard
-    const uint64_t end = (uint64_t)(W - 1) * a.ps + (uint64_t)(tile + 1) * (WG * LB);
-    bool full = (uint64_t)(tile + 1) * (WG * LB) <= a.ps;
-    for (int j = 0; j < a.K; ++j) full = full && end <= a.in[j].valid;
-#pragma unroll
-    for (int i = 0; i < R; ++i) full = full && end <= a.out[i].valid;
-    if (full) {
-      gfbit_body<W, R, LW, ACC, PFD, CEIL, KR, true>(a, obj, off);
-      return;
-    }
-  }
-  gfbit_body<W, R, LW, ACC, PFD, CEIL, KR, false>(a, obj, off);
 }
 
 // ===========================================================================

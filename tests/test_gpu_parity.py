@@ -276,8 +276,7 @@ def test_device_roundtrip_bench_shape(gpu, le):
                                  {"LEOEC_GFBIT_CBM": "1"}, {"LEOEC_GFBIT_CBM": "2"},
                                  {"LEOEC_GFBIT_CBM": "3"}, {"LEOEC_GFBIT_CBM": "4"},
                                  {"LEOEC_GFBIT_CBM": "5"},
-                                 {"LEOEC_GFBIT_FORM": "2"},  # gfbx_apply (LDS-shared, split rows)
-                                 {"LEOEC_GFBIT_FAST": "1"}],  # full-tile fast path
+                                 {"LEOEC_GFBIT_FORM": "2"}],  # gfbx_apply (LDS-shared, split rows)
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_cauchy_kernel_forms_agree(gpu, le, oracle, env, measure):
     """cauchyrs through the generic masked-bitmatrix kernel and through every
