@@ -153,6 +153,45 @@ def test_single_rank_cpu_leg_checks_parity(monkeypatch):
     assert cb["cores"] >= 1 and cb["host_cpus"] >= cb["cores"] and cb["affinity_cpus"] >= 1
 
 
+class WithCeiling(CpuBackend):
+    calls = []
+
+    def pattern_ceiling(self, objs, size, parity, enc_bytes):
+        WithCeiling.calls.append((objs.shape[0], size, enc_bytes))
+        return {"achieved": 1.0, "shipped_over_ceiling": 0.5}
+
+
+class BrokenCeiling(CpuBackend):
+    def pattern_ceiling(self, objs, size, parity, enc_bytes):
+        raise RuntimeError("no measurement build")
+
+
+def test_single_rank_pattern_ceiling_leg(monkeypatch):
+    """The live pattern-ceiling leg runs once at N = 1 after the timed region
+    (on the rank's batch and its encode bytes) and lands in `roofline`; a
+    failing leg is recorded and never fails the measurement."""
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    argv = ["--objects", "3", "--no-cpu"] + SMALL
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        rc = bench.main(argv, backend=WithCeiling)
+    rec = json.loads(out.getvalue())
+    assert rc == 0 and rec["verified"] is True
+    assert rec["roofline"]["pattern_ceiling"] == {"achieved": 1.0, "shipped_over_ceiling": 0.5}
+    assert WithCeiling.calls == [(3, 65536, rec["roofline"]["alg_bytes_per_launch"])]
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        rc = bench.main(argv, backend=BrokenCeiling)
+    rec = json.loads(out.getvalue())
+    assert rc == 0 and rec["verified"] is True
+    assert rec["roofline"]["pattern_ceiling"]["achieved"] is None
+    assert "no measurement build" in rec["roofline"]["pattern_ceiling"]["error"]
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        bench.main(argv + ["--no-ceiling"], backend=WithCeiling)
+    assert "pattern_ceiling" not in json.loads(out.getvalue())["roofline"]
+
+
 def test_single_rank_wrong_parity_fails(monkeypatch):
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     argv = ["--objects", "3", "--cpu-seconds", "0.01", "--cpu-objects", "2"] + SMALL
