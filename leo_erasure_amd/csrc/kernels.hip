@@ -294,8 +294,6 @@ template <int W>
 LibDecFn lib_dec_kernel_w() {
 #ifdef LEOEC_MEASURE
   if (lib_dec_lanes() == 64) return &detail::lib_dec_apply<W, 64>;
-  if (knobs().lib_dec_la == 4) return &detail::lib_dec_apply<W, kThreads, 4>;
-  if (knobs().lib_dec_la == 6) return &detail::lib_dec_apply<W, kThreads, 6>;
 #endif
   return &detail::lib_dec_apply<W>;
 }

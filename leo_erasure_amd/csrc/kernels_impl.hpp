@@ -735,9 +735,7 @@ struct LibDecArgs {
 constexpr int lib_dec_waves(int w) { return w <= 5 ? 4 : w <= 11 ? 3 : 2; }
 
 // TW: lanes per workgroup = 16-byte columns per tile (as lib_apply).
-// LA: packets of load look-ahead (shipped 2; other depths are measurement
-// forms, LEOEC_LIB_DEC_LA).
-template <int W, int TW = kThreads, int LA = 2>
+template <int W, int TW = kThreads>
 __global__ void __launch_bounds__(TW) __attribute__((amdgpu_waves_per_eu(lib_dec_waves(W), 8)))
 lib_dec_apply(const LibDecArgs a) {
   constexpr uint32_t kTileBytes = TW * 16u;
@@ -761,7 +759,7 @@ lib_dec_apply(const LibDecArgs a) {
   // with the loads of the next LA packets in flight (as lib_apply).  Absent
   // shards (P or Q not a survivor, erased data blocks) read as zero without
   // a memory access, so the stream's register indices stay static.
-  constexpr int RS = LA + 1, NP = (W + 2) * W;
+  constexpr int LA = 2, RS = LA + 1, NP = (W + 2) * W;
   auto shard_of = [&](int blk) -> const DevShard& {  // blk: 0 P, 1 Q, 2 + j data j
     return blk < 2 ? a.cod[blk] : a.data[blk - 2];
   };

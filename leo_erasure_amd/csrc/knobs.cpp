@@ -70,7 +70,6 @@ const Knobs* read_env() {
   k->gfbit_form = env_int("LEOEC_GFBIT_FORM", k->gfbit_form);
   k->gfbit_waves = env_int("LEOEC_GFBIT_WAVES", k->gfbit_waves);
   k->gfbit_cbm = env_int("LEOEC_GFBIT_CBM", k->gfbit_cbm);
-  k->lib_dec_la = env_int("LEOEC_LIB_DEC_LA", k->lib_dec_la);
   k->gfs_mode = env_int("LEOEC_GFS_MODE", k->gfs_mode);
   k->gfs_pf = env_int("LEOEC_GFS_PF", k->gfs_pf);
   return k;

@@ -60,7 +60,6 @@ struct Knobs {
   int gfbit_waves = 0;       // LEOEC_GFBIT_WAVES=4|5: register cap (waves per SIMD), w = 8
   int gfs_pf = 1;            // LEOEC_GFS_PF=2: two inputs in flight (w = 16/32, 4 rows)
   int gfs_mode = 0;          // LEOEC_GFS_MODE=1|2: w = 32 timing forms (not a code)
-  int lib_dec_la = 2;        // LEOEC_LIB_DEC_LA=4|6: lib_dec_apply look-ahead (packets)
   int gfbit_cbm = 0;         // LEOEC_GFBIT_CBM: cauchyrs(10,4,8) encode with its bitmatrix compiled
                              //   in (cbm_inst.hip): 0 off, 1 64 lanes 2 waves 16 packets in flight, 2 the same
                              //   with 10, 3 128 lanes, 4 64 lanes 3 waves 4 in flight, 5 256 lanes

@@ -309,7 +309,7 @@ def test_bitmatrix_kernel_forms_agree(gpu, le, oracle, form, measure):
         assert st == "ok" and rep == [blocks[0], blocks[k]]
 
 
-@pytest.mark.parametrize("form", ["0", "1", "1-wg256", "1-la4", "1-decwg64", "1-decla4", "1-decla6"])
+@pytest.mark.parametrize("form", ["0", "1", "1-wg256", "1-la4", "1-decwg64"])
 def test_liberation_encode_forms(gpu, le, oracle, form, measure):
     """lib_apply (the liberation bitmatrix structure compiled in, LEOEC_LIB_FORM=1,
     shipped with 64-lane, 1 KiB tiles; "1-wg256": the 256-lane, 4 KiB-tile
@@ -324,8 +324,6 @@ def test_liberation_encode_forms(gpu, le, oracle, form, measure):
         measure.setenv("LEOEC_LIB_LA", "4")
     if form.endswith("decwg64"):
         measure.setenv("LEOEC_LIB_DEC_WG", "64")
-    if "decla" in form:
-        measure.setenv("LEOEC_LIB_DEC_LA", form[-1])
     for w in (3, 5, 7, 11, 13):
         for k in sorted({1, 2, (w + 1) // 2, w}):
             for size in (1, 4097, 150001):
