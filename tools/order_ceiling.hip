@@ -42,6 +42,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int K = 10, R = 4;
 struct Geo {
   unsigned bs;
+  unsigned long long spacing;  // bytes from data block j to j+1 (bs = the reference's layout)
   unsigned long long obj;
   unsigned nobj;
   unsigned tiles;  // tiles per block
@@ -116,7 +117,7 @@ __global__ void __launch_bounds__(WG) pattern(const unsigned char* __restrict__ 
   if (off >= BS) return;
   u32x4 d[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) d[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(ib + (size_t)j * BS), off, 0, 2);
+  for (int j = 0; j < K; ++j) d[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(ib + (size_t)j * geo.spacing), off, 0, 2);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     u32x4 acc = d[r];
@@ -145,13 +146,18 @@ int main(int argc, char** argv) {
   const unsigned long long osz = argc > 1 ? strtoull(argv[1], nullptr, 10) : (64ull << 20);
   const unsigned nobj = argc > 2 ? (unsigned)atoi(argv[2]) : 64u;
   const int reps = argc > 3 ? atoi(argv[3]) : 20;
+  // diagnostic only (argv[4]): extra bytes between consecutive data blocks,
+  // i.e. NOT the reference's layout; argv[5] = "quick": tile-major orders only
+  const unsigned long long pad = argc > 4 ? strtoull(argv[4], nullptr, 10) : 0ull;
+  const bool quick = argc > 5 && std::string(argv[5]) == "quick";
   Geo G{};
   G.bs = (unsigned)(((osz + 8 * K - 1) / (8 * K) + 15) / 16 * 16 * 8);
-  G.obj = osz;
+  G.spacing = G.bs + pad;
+  G.obj = pad ? (unsigned long long)K * G.spacing : osz;
   G.nobj = nobj;
-  printf("# object %llu B, bs %u, %u objects\n", osz, G.bs, nobj);
+  printf("# object %llu B, bs %u, block spacing %llu, %u objects\n", osz, G.bs, G.spacing, nobj);
   unsigned char *in, *out;
-  const size_t in_bytes = (size_t)nobj * osz + (size_t)K * G.bs;
+  const size_t in_bytes = (size_t)nobj * G.obj + (size_t)K * G.spacing;
   const size_t out_bytes = (size_t)nobj * R * G.bs;
   CHECK(hipMalloc(&in, in_bytes));
   CHECK(hipMalloc(&out, out_bytes));
@@ -163,6 +169,7 @@ int main(int argc, char** argv) {
   for (unsigned wg : {64u, 256u}) {
     const std::string w = " wg" + std::to_string(wg);
     cases.push_back({"tile-major" + w, wg, 0, 1});
+    if (quick) continue;
     cases.push_back({"object-major" + w, wg, 1, 1});
     cases.push_back({"xcd objects" + w, wg, 3, 1});
     cases.push_back({"xcd segments" + w, wg, 4, 1});
