@@ -47,6 +47,7 @@ struct Geo {
   unsigned nobj;
   unsigned tiles;  // tiles per block
   unsigned order, chunk;
+  unsigned skew;  // diagnostic: blocks K/2..K-1 read `skew` bytes further along than blocks 0..K/2-1
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
@@ -117,7 +118,11 @@ __global__ void __launch_bounds__(WG) pattern(const unsigned char* __restrict__ 
   if (off >= BS) return;
   u32x4 d[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) d[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(ib + (size_t)j * geo.spacing), off, 0, 2);
+  for (int j = 0; j < K; ++j) {
+    // (skew: a pattern experiment, the XOR then mixes columns — not a code)
+    const unsigned o = j >= K / 2 && geo.skew ? (off + geo.skew) % BS : off;
+    d[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(ib + (size_t)j * geo.spacing), o, 0, 2);
+  }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     u32x4 acc = d[r];
@@ -150,9 +155,12 @@ int main(int argc, char** argv) {
   // i.e. NOT the reference's layout; argv[5] = "quick": tile-major orders only
   const unsigned long long pad = argc > 4 ? strtoull(argv[4], nullptr, 10) : 0ull;
   const bool quick = argc > 5 && std::string(argv[5]) == "quick";
+  const unsigned skew = argc > 6 ? (unsigned)strtoul(argv[6], nullptr, 10) : 0u;
   Geo G{};
   G.bs = (unsigned)(((osz + 8 * K - 1) / (8 * K) + 15) / 16 * 16 * 8);
   G.spacing = G.bs + pad;
+  G.skew = skew;
+  if (skew) printf("# blocks %d..%d read %u bytes further along (pattern experiment)\n", K / 2, K - 1, skew);
   G.obj = pad ? (unsigned long long)K * G.spacing : osz;
   G.nobj = nobj;
   printf("# object %llu B, bs %u, block spacing %llu, %u objects\n", osz, G.bs, G.spacing, nobj);
