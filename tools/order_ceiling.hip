@@ -120,7 +120,10 @@ __global__ void __launch_bounds__(WG) pattern(const unsigned char* __restrict__ 
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     // (skew: a pattern experiment, the XOR then mixes columns — not a code)
-    const unsigned o = j >= K / 2 && geo.skew ? (off + geo.skew) % BS : off;
+    // skew 1: the 1 KiB windows of a pair swap (off ^ 1024), else a shift
+    const unsigned o = j >= K / 2 && geo.skew
+                           ? (geo.skew == 1u ? ((off ^ 1024u) < BS ? off ^ 1024u : off) : (off + geo.skew) % BS)
+                           : off;
     d[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(ib + (size_t)j * geo.spacing), o, 0, 2);
   }
 #pragma unroll
