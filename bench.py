@@ -150,7 +150,7 @@ class GpuBackend:
         lib = self.le._lib
         if not os.path.exists(lib.MEASURE_LIB_PATH):
             return {"achieved": None, "error": "measurement build absent (make -C leo_erasure_amd/csrc measure)"}
-        mlib = lib._load(lib.MEASURE_LIB_PATH)
+        mlib = lib.measure_library()
         stream = self.torch.cuda.current_stream().cuda_stream
         n = objs.shape[0]
 

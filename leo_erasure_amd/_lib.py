@@ -120,6 +120,15 @@ def use_library(path):
     return prev
 
 
+def measure_library():
+    """The measurement build (libleoec_measure.so), loaded beside whatever
+    library is in use, for its measurement-only entry points
+    (leoec_measure_xor_pattern_dev); raises if it was not built."""
+    if not os.path.exists(MEASURE_LIB_PATH):
+        raise RuntimeError(f"{MEASURE_LIB_PATH} not built (make -C leo_erasure_amd/csrc measure)")
+    return _load(MEASURE_LIB_PATH)
+
+
 def is_measure_build():
     return hasattr(_current, "leoec_measure_reload")
 
