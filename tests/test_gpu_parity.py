@@ -482,34 +482,6 @@ def test_cauchy_aligned_copy_batches(gpu, le, oracle, measure, env):
         assert gpu.equal(objs, ref), (k, m, size)
 
 
-def test_gf8_pair_swap_variant(gpu, le, oracle, measure):
-    """gf8 variant 47 (measurement build): pair-swapped block halves with the
-    half-sums handed over through LDS.  Encode parity identical to the
-    shipped kernel's (and the oracle's for some objects), decode in place,
-    on whole, ragged and 64 MiB objects."""
-    k, m, w = 10, 4, 8
-    for n, size in [(9, 1048576), (7, 1048576 - 333), (5, 3 * 1048576 + 4321), (2, 67108864)]:
-        bs, _ = le.layout("vandrs", (k, m, w), size)
-        host, objs = _batch(gpu, n, size, max(k, m) * bs, 5 + size % 97)
-        ref = objs.clone()
-        outs = []
-        for var in ("0", "47"):
-            measure.setenv("LEOEC_GF8_VARIANT", var)
-            parity = gpu.full((n, m * bs), 0x5A, dtype=gpu.uint8, device="cuda")
-            le.device.encode("vandrs", (k, m, w), objs, size, parity)
-            gpu.cuda.synchronize()
-            outs.append(parity.cpu().numpy())
-        assert np.array_equal(outs[0], outs[1]), size
-        if size < (1 << 24):
-            r = oracle.encode("vandrs", k, m, w, host[0, :size].tobytes())
-            assert outs[1][0, :m * bs].tobytes() == b"".join(r[k:]), size
-        objs[:, :4 * bs] = 0
-        le.device.decode("vandrs", (k, m, w), objs, size, gpu.from_numpy(outs[1]).cuda(),
-                         [0, 1, 2, 3])
-        gpu.cuda.synchronize()
-        assert gpu.equal(objs, ref), size
-
-
 @pytest.mark.parametrize("tgroup", ["5", "128"])
 def test_gf8_segment_map_forms(gpu, le, oracle, measure, tgroup):
     """gf8 tile map 4 (XCD-interleaved runs of consecutive tiles, shipped for
