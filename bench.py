@@ -198,7 +198,13 @@ class GpuBackend:
 
 # ---------------------------------------------------------------------------
 def cpu_share():
-    """Threads the CPU baseline may use on this host, and what that rests on."""
+    """Worker threads the CPU baseline may use on this host, and what that
+    rests on.  The share is the cgroup's cpu.max quota (whole CPUs) or, with
+    no quota, the affinity mask capped at the GPU box's per-GPU share; one
+    CPU of it is left to the process's other threads (main, torch, HIP
+    runtime): with workers = quota they compete with those for the quota and
+    the cgroup's CFS bandwidth control throttles whole passes (round 3's
+    driver run lost 0.88 s to it)."""
     host = os.cpu_count() or 1
     try:
         aff = len(os.sched_getaffinity(0))
@@ -213,12 +219,20 @@ def cpu_share():
     except (OSError, ValueError):
         quota = None
     if quota:
-        threads, basis = max(1, min(aff, int(math.floor(quota)))), "cgroup cpu.max quota"
+        share, basis = min(aff, int(math.floor(quota))), "cgroup cpu.max quota"
     else:
-        threads, basis = min(aff, BOX_CPU_SHARE), (
+        share, basis = min(aff, BOX_CPU_SHARE), (
             f"affinity, capped at {BOX_CPU_SHARE} = the GPU box's CPU share per GPU")
+    threads = headroom_workers(share)
     return threads, {"host_cpus": host, "affinity_cpus": aff, "cgroup_cpus": quota,
-                     "threads_basis": basis}
+                     "threads_basis": basis, "share_cpus": share,
+                     "reserved_cpus": share - threads}
+
+
+def headroom_workers(share):
+    """Workers for a share of `share` whole CPUs: one CPU is left for the
+    process's own threads whenever the share has more than one."""
+    return max(1, share - 1)
 
 
 def _cpu_list(text):
@@ -326,13 +340,41 @@ def _cgroup_throttled_us():
     return None
 
 
-def cpu_baseline(objs, parity, size, n_sample, target_s):
+THROTTLE_EPS_S = 1e-3  # a pass the cgroup throttled for longer than this is flagged
+
+
+def summarize_passes(rates, throttled):
+    """Median GiB/s of a baseline's passes, over the passes the cgroup did
+    not throttle when at least 3 of them were not (throttling only ever slows
+    a pass), otherwise over all; with the spreads of the passes used."""
+    flagged = [t is not None and t > THROTTLE_EPS_S for t in throttled] if throttled else []
+    flagged += [False] * (len(rates) - len(flagged))
+    clean = [r for r, f in zip(rates, flagged) if not f]
+    used = sorted(clean if len(clean) >= 3 else rates)
+    med = used[len(used) // 2]
+    return {
+        "value": round(med, 3),
+        "passes_used": "unthrottled" if len(clean) >= 3 else "all (fewer than 3 unthrottled)",
+        "throttled_passes": sum(flagged),
+        "best_pass_GiBps": round(used[-1], 3),
+        "pass_spread": round((used[-1] - used[0]) / med, 4) if med else None,
+        "iqr_spread": round((used[(3 * len(used)) // 4] - used[len(used) // 4]) / med, 4)
+        if med else None,
+    }
+
+
+def cpu_baseline(objs, parity, size, n_sample, target_s, ref_structure_s=None):
     """The CPU restatement with ISA-L's split-table / GFNI technique
-    (oracle/leoec_oracle.c orc_bench_rs8), timed on this host's cores over a
-    bounded sample of the SAME workload: the first `n_sample` objects of rank
-    0's batch, copied to host memory.  Its encode output is also compared
-    byte for byte with the GPU's parity of those objects (outside the timed
-    region), so the line's `verified` covers encode parity too."""
+    (oracle/leoec_oracle.c orc_bench_rs8_pinned, structure 0), timed on this
+    host's cores over a bounded sample of the SAME workload: the first
+    `n_sample` objects of rank 0's batch, copied to host memory.  Its encode
+    output is also compared byte for byte with the GPU's parity of those
+    objects (outside the timed region), so the line's `verified` covers
+    encode parity too.  Then, as a second labelled figure, the reference's
+    own CPU structure (Jerasure's per-(row, input) region passes with
+    destination read-modify-write, rscoding.cpp:71 / :147; structure 1) on
+    the same sample, workers and parity check, for `ref_structure_s`
+    seconds (default target_s / 2)."""
     import numpy as np
 
     from oracle import oracle as O
@@ -343,51 +385,65 @@ def cpu_baseline(objs, parity, size, n_sample, target_s):
     n = min(n_sample, objs.shape[0])
     host = objs[:n].to("cpu", copy=True).numpy()
     gpu_par = parity[:n].to("cpu", copy=True).numpy()
-    cpu_par = np.zeros_like(gpu_par)
-    # one pool of workers for the whole baseline, worker t pinned to cpus[t],
-    # each first-touching its own slice of the sample (NUMA-local pages);
-    # passes of >= target/12 s each (several encode+decode rounds between
-    # barriers); value = the median pass.  cpu_par receives the workers'
-    # encode of the sample, compared with the GPU's parity after the clock.
-    pass_s = target_s / 12.0
-    thr0 = _cgroup_throttled_us()
-    snap0 = _cpu_snap()
-    t0 = time.perf_counter()
-    rates = O.bench_rs8_pinned(K, M, host, size, ERASED, threads, cpus, pass_s, target_s,
-                               min_passes=3, parity_out=cpu_par)
-    t_all = time.perf_counter() - t0
-    busy = _busy_between(snap0, _cpu_snap())
-    thr1 = _cgroup_throttled_us()
-    passes = [round(r, 2) for r in rates]
-    parity_ok = bool(np.array_equal(cpu_par, gpu_par))
-    rates.sort()
-    med = rates[len(rates) // 2]
-    rec = {
-        "value": round(med, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+
+    def leg(structure, total_s):
+        cpu_par = np.zeros_like(gpu_par)
+        # one pool of workers for the whole leg, worker t pinned to cpus[t],
+        # each first-touching its own slice of the sample (NUMA-local pages);
+        # passes of >= total/12 s each (several encode+decode rounds between
+        # barriers); cpu_par receives the workers' encode of the sample,
+        # compared with the GPU's parity after the clock
+        pass_s = total_s / 12.0
+        thr0 = _cgroup_throttled_us()
+        snap0 = _cpu_snap()
+        throttled = []
+        t0 = time.perf_counter()
+        rates = O.bench_rs8_pinned(K, M, host, size, ERASED, threads, cpus, pass_s, total_s,
+                                   min_passes=3, parity_out=cpu_par, structure=structure,
+                                   throttled=throttled)
+        t_all = time.perf_counter() - t0
+        busy = _busy_between(snap0, _cpu_snap())
+        thr1 = _cgroup_throttled_us()
+        rec = summarize_passes(rates, throttled)
+        rec.update({
+            "unit": "GiB/s",
+            "passes_GiBps": [round(r, 2) for r in rates],
+            "throttled_s_per_pass": [None if t is None else round(t, 4) for t in throttled],
+            "cgroup_throttled_s": None if thr0 is None or thr1 is None else
+            round((thr1 - thr0) / 1e6, 3),
+            # the host is shared: CPUs busy during the leg, ours included
+            # (the workers' `threads`), as a record of the other tenants' load
+            "host_busy_cpus": round(sum(busy.values()), 1) if busy else None,
+            "parity_vs_gpu": {"objects": n, "equal": bool(np.array_equal(cpu_par, gpu_par))},
+            "sample": f"{len(rates)} passes of >= {pass_s:.2f} s over the first {n} x {size} B "
+                      f"objects of rank 0's batch: vandrs RS({K},{M},8) encode + in-place "
+                      f"decode of data blocks {ERASED}, {threads} threads pinned one per "
+                      f"physical core, each first-touching its own slice, {t_all:.2f} s; "
+                      f"value = median pass",
+        })
+        return rec
+
+    rec = leg(0, target_s)
+    rec.update({
+        "cores": threads, "kind": "port",
         "simd": {0: "scalar", 2: "avx2-pshufb (ISA-L split tables)",
                  3: "avx512-gfni (ISA-L gf2p8affine)"}.get(O.simd_level(), "scalar"),
-        "sample": f"{len(rates)} passes of >= {pass_s:.2f} s over the first {n} x {size} B objects "
-                  f"of rank 0's batch: "
-                  f"vandrs RS({K},{M},8) encode + in-place decode of data blocks {ERASED}, "
-                  f"{threads} threads pinned one per physical core, each first-touching its "
-                  f"own slice, {t_all:.2f} s; value = median pass",
+        "structure": "ISA-L ec_encode_data: one pass per object, every output row at once",
         "pinning": {"cpus": cpus, "numa_nodes": nodes, "first_touch": "per worker thread",
                     "choice": "least busy physical cores of one NUMA node (/proc/stat)"},
-        "cgroup_throttled_s": None if thr0 is None or thr1 is None else
-        round((thr1 - thr0) / 1e6, 3),
-        "passes_GiBps": passes,
-        # the host is shared: CPUs busy during the baseline, ours included
-        # (the workers' `threads`), as a record of the other tenants' load
-        "host_busy_cpus": round(sum(busy.values()), 1) if busy else None,
-        # other tenants only ever slow a pass down: the best pass is the rate
-        # with the least interference (the value stays the median)
-        "best_pass_GiBps": round(rates[-1], 3),
-        "pass_spread": round((rates[-1] - rates[0]) / med, 4) if med else None,
-        "iqr_spread": round((rates[(3 * len(rates)) // 4] - rates[len(rates) // 4]) / med, 4)
-        if med else None,
-        "parity_vs_gpu": {"objects": n, "equal": parity_ok},
-    }
+        "workers": threads,
+    })
     rec.update(share)
+    rs = leg(1, target_s / 2.0 if ref_structure_s is None else ref_structure_s)
+    rs.update({
+        "cores": threads, "kind": "port",
+        "simd": "avx2-pshufb (gf-complete w=8 split tables)" if O.simd_level() >= 2 else "scalar",
+        "structure": ("Jerasure jerasure_matrix_encode / decode_data: per coding row, the "
+                      "coefficient-1 inputs copied / xor-ed, then one region multiply pass per "
+                      "other input over the whole block with destination read-modify-write "
+                      "(rscoding.cpp:71, :147)"),
+    })
+    rec["reference_structure"] = rs
     return rec
 
 
@@ -529,6 +585,21 @@ def run_rank(args, be, rank, world, dist=None):
     enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
     traffic, traffic_src = read_traffic(args.traffic, n, size, getattr(be, "lib_path", None))
+
+    def rank_frac(r, per_obj, ms):
+        return (r["objects"][1] - r["objects"][0]) * per_obj / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+
+    # the whole node: every rank's algorithmic bytes per launch over the
+    # slowest rank's average launch, against world x the per-GPU peak
+    agg = {}
+    for op, per_obj, key in (("encode", (K + M) * bs, "enc_ms"),
+                             ("decode", (K + len(ERASED)) * bs, "dec_ms")):
+        tot = sum((r["objects"][1] - r["objects"][0]) * per_obj for r in allr)
+        slow = max(r[key] for r in allr)
+        gbs = tot / (slow * 1e-3) / 1e9
+        agg[op] = {"alg_bytes_per_launch": tot, "slowest_rank_launch_ms": round(slow, 4),
+                   "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS * world,
+                   "frac": round(gbs / (HBM_PEAK_GBS * world), 4)}
     strong = global_n is not None
     rec = {
         "metric": METRIC_64 if strong else METRIC,
@@ -562,6 +633,10 @@ def run_rank(args, be, rank, world, dist=None):
             "alg_bytes_per_launch": enc_bytes, "avg_launch_ms": round(enc_ms, 4),
             "decode": {"achieved": round(dec_gbs, 1), "frac": round(dec_gbs / HBM_PEAK_GBS, 4),
                        "alg_bytes_per_launch": dec_bytes, "avg_launch_ms": round(dec_ms, 4)},
+            "scope": "rank 0's GPU (achieved / frac); `aggregate`: all ranks",
+            "aggregate": dict(agg, n_gpus=world,
+                              what="sum over ranks of algorithmic bytes per launch / the "
+                                   "slowest rank's average launch; peak = n_gpus x 8 TB/s"),
         },
         "kernel_ms": {
             "encode_min_med_max": [round(x, 4) for x in (min(enc_t), sorted(enc_t)[len(enc_t) // 2],
@@ -571,6 +646,8 @@ def run_rank(args, be, rank, world, dist=None):
         "per_rank": [{"rank": r["rank"], "device": r["device"], "objects": r["objects"],
                       "elapsed_s": round(r["elapsed_s"], 5),
                       "encode_ms": round(r["enc_ms"], 4), "decode_ms": round(r["dec_ms"], 4),
+                      "encode_frac": round(rank_frac(r, (K + M) * bs, r["enc_ms"]), 4),
+                      "decode_frac": round(rank_frac(r, (K + len(ERASED)) * bs, r["dec_ms"]), 4),
                       "checks": r["checks"]} for r in allr],
         "cpu_baseline": None,
     }
@@ -581,8 +658,11 @@ def run_rank(args, be, rank, world, dist=None):
         except Exception as e:  # a host problem must not discard the GPU measurement
             cb = {"value": None, "error": f"{type(e).__name__}: {e}"}
         rec["cpu_baseline"] = cb
-        if "parity_vs_gpu" in cb:
-            verified = verified and cb["parity_vs_gpu"]["equal"]
+        checked = [c for c in (cb, cb.get("reference_structure") or {}) if "parity_vs_gpu" in c]
+        rec["cpu_parity_checked"] = bool(checked)
+        verified = verified and all(c["parity_vs_gpu"]["equal"] for c in checked)
+    else:
+        rec["cpu_parity_checked"] = False
     if world == 1 and not args.no_ceiling and hasattr(be, "pattern_ceiling"):
         # after the CPU leg: this overwrites parity
         try:

@@ -16,8 +16,9 @@ except Exception:  # pragma: no cover - torch is optional for the host API
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libleoec.so")
 # The measurement build (every A/B kernel form, LEOEC_* knobs read once at
-# first use): `make -C leo_erasure_amd/csrc measure`.  Tools select it with
-# LEOEC_LIBRARY=measure; the form-parity tests switch to it with use_library().
+# first use, or set with measure_set_knob): `make -C leo_erasure_amd/csrc
+# measure`.  Tools and the form-parity tests' own process select it with
+# LEOEC_LIBRARY=measure, so a process loads one HIP library.
 MEASURE_LIB_PATH = os.path.join(_HERE, "libleoec_measure.so")
 
 CAUCHYRS, VANDRS, LIBERATION, ISARS = 1, 2, 3, 4
@@ -84,6 +85,10 @@ def _load(path=LIB_PATH):
     if hasattr(L, "leoec_measure_reload"):
         L.leoec_measure_reload.argtypes = []
         L.leoec_measure_reload.restype = None
+        L.leoec_measure_set_knob.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.leoec_measure_set_knob.restype = ctypes.c_int
+        L.leoec_measure_reset_knobs.argtypes = []
+        L.leoec_measure_reset_knobs.restype = None
     if hasattr(L, "leoec_measure_xor_pattern_dev"):  # measurement build (xor_pattern.hip)
         L.leoec_measure_xor_pattern_dev.argtypes = [
             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
@@ -133,11 +138,32 @@ def is_measure_build():
     return hasattr(_current, "leoec_measure_reload")
 
 
-def measure_reload():
-    """Measurement build only: re-read the LEOEC_* knobs from the environment."""
+def _need_measure():
     if not is_measure_build():
         raise RuntimeError(f"{library_path()} is the product build: it has no LEOEC_* knobs")
+
+
+def measure_reload():
+    """Measurement build only: re-read the LEOEC_* knobs from the environment."""
+    _need_measure()
     _current.leoec_measure_reload()
+
+
+def measure_set_knob(name, value):
+    """Measurement build only: set knob `name` (LEOEC_*) to `value`, or drop
+    its override with None; the library never reads a changed environment,
+    so nothing calls setenv while its threads run."""
+    _need_measure()
+    rc = _current.leoec_measure_set_knob(name.encode(),
+                                         None if value is None else str(value).encode())
+    if rc != 0:
+        raise ValueError(f"not a knob: {name}")
+
+
+def measure_reset_knobs():
+    """Measurement build only: drop every measure_set_knob override."""
+    _need_measure()
+    _current.leoec_measure_reset_knobs()
 
 
 def strerror(code):

@@ -4,7 +4,9 @@
 #ifdef LEOEC_MEASURE
 #include <atomic>
 #include <cstdlib>
+#include <map>
 #include <mutex>
+#include <string>
 #include <string_view>
 #endif
 
@@ -21,15 +23,30 @@ const Knobs& knobs() {
 
 namespace {
 
+// Overrides set through leoec_measure_set_knob (the form-parity tests):
+// they take precedence over the environment, which is only read, never
+// written, so no test mutates the process environment while library or HIP
+// runtime threads run.  Guarded by g_mu.
+std::map<std::string, std::string>& overrides() {
+  static auto* m = new std::map<std::string, std::string>;
+  return *m;
+}
+
+const char* lookup(const char* name) {
+  const auto& o = overrides();
+  const auto it = o.find(name);
+  return it != o.end() ? it->second.c_str() : std::getenv(name);
+}
+
 int env_int(const char* name, int dflt) {
-  const char* e = std::getenv(name);
+  const char* e = lookup(name);
   return e ? std::atoi(e) : dflt;
 }
 
 const Knobs* read_env() {
   Knobs* k = new Knobs;
   k->bitmatrix = env_int("LEOEC_BITMATRIX", k->bitmatrix);
-  if (const char* e = std::getenv("LEOEC_HOST_STAGING")) {
+  if (const char* e = lookup("LEOEC_HOST_STAGING")) {
     const std::string_view v(e);
     k->host_staging = v == "pageable" ? 1 : v == "gather" ? 2 : v == "pinned" ? 3
                       : v == "zerocopy" ? 4 : 0;
@@ -48,7 +65,7 @@ const Knobs* read_env() {
   k->hostq_fail_bs = env_int("LEOEC_HOSTQ_FAIL_BS", k->hostq_fail_bs);
   k->gf8_variant = env_int("LEOEC_GF8_VARIANT", k->gf8_variant);
   k->gf8_tmap = env_int("LEOEC_GF8_TMAP", k->gf8_tmap);
-  k->gf8_tmap_set = std::getenv("LEOEC_GF8_TMAP") != nullptr;
+  k->gf8_tmap_set = lookup("LEOEC_GF8_TMAP") != nullptr;
   k->gf8_wg = env_int("LEOEC_GF8_WG", k->gf8_wg);
   k->gf8_tgroup = env_int("LEOEC_GF8_TGROUP", k->gf8_tgroup);
   k->gfw_form = env_int("LEOEC_GFW_FORM", k->gfw_form);
@@ -94,11 +111,34 @@ const Knobs& knobs() {
 
 }  // namespace leoec
 
-// Measurement build only: re-read the LEOEC_* variables (a test that changes
-// one between calls).  Earlier snapshots stay valid (they are never freed),
-// so a concurrent launch sees either the old or the new set.
+// Measurement build only: re-read the LEOEC_* variables and overrides.
+// Earlier snapshots stay valid (they are never freed), so a concurrent launch
+// sees either the old or the new set.
 extern "C" __attribute__((visibility("default"))) void leoec_measure_reload(void) {
   std::lock_guard<std::mutex> lock(leoec::g_mu);
+  leoec::g_knobs.store(leoec::read_env(), std::memory_order_release);
+}
+
+// Measurement build only: set knob `name` (an LEOEC_* name) to `value`, or
+// drop its override with value == NULL (the environment's value, if any,
+// applies again), and publish a new snapshot.  Returns 0, or -1 for a name
+// that is not an LEOEC_* knob.
+extern "C" __attribute__((visibility("default"))) int leoec_measure_set_knob(const char* name,
+                                                                            const char* value) {
+  if (!name || std::string_view(name).rfind("LEOEC_", 0) != 0) return -1;
+  std::lock_guard<std::mutex> lock(leoec::g_mu);
+  if (value)
+    leoec::overrides()[name] = value;
+  else
+    leoec::overrides().erase(name);
+  leoec::g_knobs.store(leoec::read_env(), std::memory_order_release);
+  return 0;
+}
+
+// Measurement build only: drop every override set by leoec_measure_set_knob.
+extern "C" __attribute__((visibility("default"))) void leoec_measure_reset_knobs(void) {
+  std::lock_guard<std::mutex> lock(leoec::g_mu);
+  leoec::overrides().clear();
   leoec::g_knobs.store(leoec::read_env(), std::memory_order_release);
 }
 

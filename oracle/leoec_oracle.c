@@ -14,6 +14,7 @@
 #include "leoec_oracle.h"
 
 #include <pthread.h>
+#include <stdio.h>
 #include <sched.h>
 #include <time.h>
 #include <stdlib.h>
@@ -817,7 +818,81 @@ typedef struct {
   const uint64_t *mats; /* GFNI affine matrices, nout x k */
   const int *want;      /* decode: erased data ids */
   const int *surv;      /* decode: survivor ids */
+  const uint32_t *coef; /* nout x k coefficients (structure 1: ones are copies / xors) */
+  int structure;        /* 0: one pass over all rows (ISA-L ec_encode_data);
+                           1: Jerasure's per-(row, input) region passes */
 } bench_job;
+
+/* Jerasure's structure (jerasure_matrix_encode -> jerasure_matrix_dotprod per
+ * coding row, rscoding.cpp:71; jerasure_matrix_decode_data per erased row,
+ * rscoding.cpp:147): for each output row, first the inputs whose coefficient
+ * is 1 (memcpy for the first, galois_region_xor after), then one
+ * galois_w08_region_multiply pass per other nonzero coefficient, each over
+ * the whole block, accumulating into the destination from the second pass
+ * on (read-modify-write).  The multiply is gf-complete's w = 8 split-table
+ * technique (two 16-entry nibble tables and PSHUFB), here 32 B wide. */
+static void region_mul_scalar(const uint8_t *t, const uint8_t *s, uint8_t *d, uint64_t len,
+                              int add) {
+  if (add)
+    for (uint64_t i = 0; i < len; i++) d[i] ^= t[s[i] & 15] ^ t[16 + (s[i] >> 4)];
+  else
+    for (uint64_t i = 0; i < len; i++) d[i] = t[s[i] & 15] ^ t[16 + (s[i] >> 4)];
+}
+
+static void region_xor(const uint8_t *s, uint8_t *d, uint64_t len) {
+  uint64_t i = 0;
+  for (; i + 8 <= len; i += 8) {
+    uint64_t a, b;
+    memcpy(&a, s + i, 8);
+    memcpy(&b, d + i, 8);
+    a ^= b;
+    memcpy(d + i, &a, 8);
+  }
+  for (; i < len; i++) d[i] ^= s[i];
+}
+
+#if defined(__x86_64__)
+__attribute__((target("avx2"))) static void region_mul_avx2(const uint8_t *t, const uint8_t *s,
+                                                            uint8_t *d, uint64_t len, int add) {
+  const __m256i mask = _mm256_set1_epi8(0x0f);
+  const __m256i tl = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)t));
+  const __m256i th = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)(t + 16)));
+  uint64_t i = 0;
+  for (; i + 32 <= len; i += 32) {
+    const __m256i x = _mm256_loadu_si256((const __m256i *)(s + i));
+    __m256i r = _mm256_xor_si256(_mm256_shuffle_epi8(tl, _mm256_and_si256(x, mask)),
+                                 _mm256_shuffle_epi8(th, _mm256_and_si256(_mm256_srli_epi64(x, 4), mask)));
+    if (add) r = _mm256_xor_si256(r, _mm256_loadu_si256((const __m256i *)(d + i)));
+    _mm256_storeu_si256((__m256i *)(d + i), r);
+  }
+  if (i < len) region_mul_scalar(t, s + i, d + i, len - i, add);
+}
+#endif
+
+static void apply_regions(int nin, int nout, const uint32_t *coef, const uint8_t *tbl, int simd,
+                          const uint8_t *const *in, uint8_t *const *out, uint64_t len) {
+  for (int o = 0; o < nout; o++) {
+    int init = 0;
+    for (int j = 0; j < nin; j++) {
+      if (coef[o * nin + j] != 1) continue;
+      if (init) region_xor(in[j], out[o], len);
+      else memcpy(out[o], in[j], len);
+      init = 1;
+    }
+    for (int j = 0; j < nin; j++) {
+      const uint32_t c = coef[o * nin + j];
+      if (c <= 1) continue;
+      const uint8_t *t = tbl + ((size_t)o * nin + j) * 32;
+#if defined(__x86_64__)
+      if (simd >= 2) region_mul_avx2(t, in[j], out[o], len, init);
+      else
+#endif
+        region_mul_scalar(t, in[j], out[o], len, init);
+      init = 1;
+    }
+    if (!init) memset(out[o], 0, len);
+  }
+}
 
 /* One object of a bench job: RSCoding::doEncode's stripe staging, then the
  * encode, or the in-place decode of the job's erased data blocks.  `tail` is
@@ -849,6 +924,8 @@ static void bench_object_at(const bench_job *J, const uint8_t *obj, uint8_t *par
        * own (identical) bytes in the object / staged tail */
       for (int i = 0; i < J->nout; i++) out[i] = (uint8_t *)blk[J->want[i]];
     }
+    if (J->structure == 1) apply_regions(nin, J->nout, J->coef, J->tbl, J->simd, in, out, bs);
+    else
 #if defined(__x86_64__)
     if (J->simd >= 3) apply_gfni(nin, J->nout, J->mats, J->tbl, in, out, bs);
     else if (J->simd >= 2) apply_avx2(nin, J->nout, J->tbl, in, out, bs);
@@ -887,6 +964,7 @@ typedef struct {
   int nout, surv[256], want[256];
   uint8_t *tbl;   /* (m+k) x k x 32 split tables */
   uint64_t *mats; /* nout x k GFNI matrices */
+  uint32_t *coef; /* nout x k coefficients */
 } bench_plan;
 
 static int bench_plan_make(bench_plan *P, int op, int k, int m, const int *erased, int nerased) {
@@ -894,6 +972,7 @@ static int bench_plan_make(bench_plan *P, int op, int k, int m, const int *erase
   uint32_t *rows = malloc(sizeof(uint32_t) * (m + k) * k);
   P->tbl = malloc((size_t)(m + k) * k * 32);
   P->mats = NULL;
+  P->coef = NULL;
   int *surv = P->surv, *want = P->want, nout = 0;
   int rc = orc_vandermonde_coding_matrix(k, m, 8, C);
   if (rc) goto done;
@@ -920,6 +999,8 @@ static int bench_plan_make(bench_plan *P, int op, int k, int m, const int *erase
   init_tables(nout, k, rows, P->tbl);
   P->mats = malloc(sizeof(uint64_t) * (size_t)(nout ? nout : 1) * k);
   for (int i = 0; i < nout * k; i++) P->mats[i] = gfni_matrix(rows[i]);
+  P->coef = rows;
+  rows = NULL;
 done:
   free(C);
   free(rows);
@@ -930,6 +1011,7 @@ done:
 static void bench_plan_free(bench_plan *P) {
   free(P->tbl);
   free(P->mats);
+  free(P->coef);
 }
 
 int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride, uint64_t size,
@@ -957,6 +1039,7 @@ int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride
       J->o0 = (int)((long long)nobj * t / threads);
       J->o1 = (int)((long long)nobj * (t + 1) / threads);
       J->parity = parity; J->tbl = tbl; J->mats = mats; J->want = want; J->surv = surv;
+      J->coef = P.coef; J->structure = 0;
       pthread_create(&th[t], NULL, bench_worker, J);
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
@@ -974,7 +1057,11 @@ int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride
  * until total_s seconds and min_passes passes have run.  rates[i] = GiB/s of
  * object payload (2 x objects x size per round) of pass i; returns the number
  * of passes (<= max_passes) or a negative ORC_E_*.  parity_out (nobj x m x
- * bs) receives the workers' encode of the sample, for the parity check. */
+ * bs) receives the workers' encode of the sample, for the parity check.
+ * structure 0: ISA-L's one pass per object (apply_gfni / apply_avx2);
+ * structure 1: Jerasure's per-(row, input) region passes (apply_regions).
+ * throttled_s (nullable, max_passes): the cgroup's CFS-throttled seconds
+ * during each pass, -1 where cpu.stat is unreadable. */
 /* Objects are handed out from a shared counter per phase (chunks of
  * kBenchChunk), not as fixed slices: a worker whose core another tenant of
  * the host takes for a while does fewer objects instead of holding every
@@ -1064,12 +1151,26 @@ static double now_s(void) {
   return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
+/* The cgroup's cumulative CFS-throttled time in microseconds (cpu.stat
+ * throttled_usec), or -1 where unreadable. */
+static long long cgroup_throttled_us(void) {
+  FILE *f = fopen("/sys/fs/cgroup/cpu.stat", "r");
+  if (!f) return -1;
+  char key[64];
+  long long v, r = -1;
+  while (fscanf(f, "%63s %lld", key, &v) == 2)
+    if (!strcmp(key, "throttled_usec")) { r = v; break; }
+  fclose(f);
+  return r;
+}
+
 int orc_bench_rs8_pinned(int k, int m, const uint8_t *src, uint64_t src_stride, uint64_t size,
                          int nobj, const int *erased, int nerased, int threads, const int *cpus,
                          double pass_s, double total_s, int min_passes, double *rates,
-                         int max_passes, uint8_t *parity_out) {
+                         int max_passes, uint8_t *parity_out, int structure,
+                         double *throttled_s) {
   if (k <= 0 || m <= 0 || k + m > 256 || threads <= 0 || threads > 256 || nerased > m ||
-      nobj <= 0 || max_passes <= 0)
+      nobj <= 0 || max_passes <= 0 || structure < 0 || structure > 1)
     return ORC_E_PARAMS;
   uint64_t bs = orc_block_size(k, 8, size);
   bench_plan PE, PD;
@@ -1100,9 +1201,10 @@ int orc_bench_rs8_pinned(int k, int m, const uint8_t *src, uint64_t src_stride, 
     E->o0 = (int)((long long)nobj * t / threads);
     E->o1 = (int)((long long)nobj * (t + 1) / threads);
     E->tbl = PE.tbl; E->mats = PE.mats; E->want = PE.want; E->surv = PE.surv;
+    E->coef = PE.coef; E->structure = structure;
     *D = *E;
     D->op = 1; D->nout = PD.nout; D->tbl = PD.tbl; D->mats = PD.mats; D->want = PD.want;
-    D->surv = PD.surv;
+    D->surv = PD.surv; D->coef = PD.coef;
     pthread_create(&th[t], NULL, pinned_main, W);
   }
   /* round 0 (untimed): the first touch is done and the caches are warm.
@@ -1114,6 +1216,7 @@ int orc_bench_rs8_pinned(int k, int m, const uint8_t *src, uint64_t src_stride, 
   for (int t = 0; t < threads; t++) any_err |= Ws[t].err;
   double t_all = 0.0;
   while (!any_err && np < max_passes && (t_all < total_s || np < min_passes)) {
+    const long long th0 = throttled_s ? cgroup_throttled_us() : -1;
     double t0 = now_s(), dt;
     int reps = 0;
     do {
@@ -1124,6 +1227,10 @@ int orc_bench_rs8_pinned(int k, int m, const uint8_t *src, uint64_t src_stride, 
       dt = now_s() - t0;
     } while (dt < pass_s);
     t_all += dt;
+    if (throttled_s) {
+      const long long th1 = cgroup_throttled_us();
+      throttled_s[np] = th0 < 0 || th1 < 0 ? -1.0 : (double)(th1 - th0) * 1e-6;
+    }
     rates[np++] = 2.0 * (double)nobj * (double)size * reps / dt / (double)(1u << 30);
   }
   stop = 1;

@@ -106,7 +106,8 @@ int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride
 int orc_bench_rs8_pinned(int k, int m, const uint8_t *src, uint64_t src_stride, uint64_t size,
                          int nobj, const int *erased, int nerased, int threads, const int *cpus,
                          double pass_s, double total_s, int min_passes, double *rates,
-                         int max_passes, uint8_t *parity_out);
+                         int max_passes, uint8_t *parity_out, int structure,
+                         double *throttled_s);
 int orc_simd_level(void);   /* 0 scalar, 2 avx2 (PSHUFB), 3 avx512bw+gfni (affine) */
 
 #ifdef __cplusplus

@@ -15,6 +15,8 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (run with -m gpu on the MI355X box)")
+    config.addinivalue_line("markers", "measure_gpu: measurement-build form tests (GPU); run in "
+                            "their own process with LEOEC_LIBRARY=measure")
 
 
 @pytest.fixture(scope="session")
@@ -38,36 +40,35 @@ def gpu(le):
     return torch
 
 
-class MeasureEnv:
-    """LEOEC_* knobs of the measurement build: set / clear a variable and have
-    the library re-read them (the product build never reads the environment)."""
+class MeasureKnobs:
+    """LEOEC_* knobs of the measurement build, set through the library's own
+    setter (leoec_measure_set_knob): the process environment is never
+    written while the library's queue threads and the HIP runtime's threads
+    run (round 3's verdict on the round-2 abort)."""
 
-    def __init__(self, mp, lib):
-        self.mp, self.lib = mp, lib
+    def __init__(self, lib):
+        self.lib = lib
 
     def setenv(self, key, value):
-        self.mp.setenv(key, value)
-        self.lib.measure_reload()
+        self.lib.measure_set_knob(key, value)
 
     def delenv(self, key, raising=False):
-        self.mp.delenv(key, raising=False)
-        self.lib.measure_reload()
+        self.lib.measure_set_knob(key, None)
 
 
 @pytest.fixture
-def measure(le, gpu, monkeypatch):
-    """Route the package through libleoec_measure.so (A/B kernel forms) for
-    one test; skipped when that build is absent (`make -C leo_erasure_amd/csrc
-    measure`): the forms it adds are not shipped."""
+def measure(le, gpu):
+    """The measurement build's A/B kernel forms for one test.  They run only
+    in a process that loaded libleoec_measure.so alone (LEOEC_LIBRARY=measure,
+    tests/test_measure_forms.py's own process, started by
+    test_gpu_parity.py::test_measurement_forms_in_own_process): a product-test
+    process never loads a second HIP library."""
     from leo_erasure_amd import _lib
-    if not os.path.exists(_lib.MEASURE_LIB_PATH):
-        pytest.skip("measurement build absent (make -C leo_erasure_amd/csrc measure)")
-    prev = _lib.use_library(_lib.MEASURE_LIB_PATH)
+    if not _lib.is_measure_build():
+        pytest.skip("measurement-form test: runs in its own process with LEOEC_LIBRARY=measure "
+                    "(test_measurement_forms_in_own_process)")
+    _lib.measure_reset_knobs()
     try:
-        assert le.gf_init() == "ok"
-        _lib.measure_reload()
-        yield MeasureEnv(monkeypatch, _lib)
+        yield MeasureKnobs(_lib)
     finally:
-        monkeypatch.undo()
-        _lib.measure_reload()
-        _lib.use_library(prev)
+        _lib.measure_reset_knobs()

@@ -5,6 +5,7 @@ import os
 import sys
 
 import numpy as np
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -87,4 +88,56 @@ def test_pinned_baseline_queue_ragged(oracle):
                                     parity_out=par)
     oracle.bench_rs8(0, 10, 4, objs, size, size, n, ref, threads=1)
     assert len(rates) >= 3 and all(r > 0 for r in rates)
+    assert np.array_equal(par, ref)
+
+
+@pytest.mark.parametrize("share,workers", [(16, 15), (8, 7), (2, 1), (1, 1)])
+def test_headroom_rule(share, workers):
+    """A share of N whole CPUs runs N - 1 workers (at least 1): the quota's
+    last CPU is for the process's main, torch and HIP threads, so CFS
+    bandwidth control does not throttle the passes."""
+    assert bench.headroom_workers(share) == workers
+
+
+def test_cpu_share_leaves_one_cpu(tmp_path, monkeypatch):
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(64)))
+    real_open = open
+
+    def fake_open(path, *a, **k):
+        if path == "/sys/fs/cgroup/cpu.max":
+            f = tmp_path / "cpu.max"
+            f.write_text("1600000 100000\n")
+            return real_open(f, *a, **k)
+        return real_open(path, *a, **k)
+
+    monkeypatch.setattr("builtins.open", fake_open)
+    threads, share = bench.cpu_share()
+    assert share["cgroup_cpus"] == 16.0 and share["share_cpus"] == 16
+    assert threads == 15 and share["reserved_cpus"] == 1
+
+
+def test_throttled_passes_are_excluded():
+    rates = [100.0, 101.0, 60.0, 99.0, 102.0, 70.0]
+    thr = [0.0, 0.0, 0.4, 0.0, None, 0.2]
+    s = bench.summarize_passes(rates, thr)
+    assert s["throttled_passes"] == 2 and s["passes_used"] == "unthrottled"
+    assert s["value"] == 101.0  # median of 99, 100, 101, 102
+    # fewer than 3 clean passes: all passes, flagged
+    s = bench.summarize_passes([50.0, 90.0, 91.0], [0.3, 0.0, 0.2])
+    assert s["passes_used"].startswith("all") and s["value"] == 90.0
+
+
+def test_reference_structure_parity(oracle):
+    """The Jerasure-structure leg (per-(row, input) region passes) writes the
+    same parity as the one-pass leg and the oracle."""
+    n, size = 6, 200003
+    objs = np.random.default_rng(3).integers(0, 256, (n, size), dtype=np.uint8)
+    bs = oracle.block_size(10, 8, size)
+    par = np.zeros((n, 4 * bs), np.uint8)
+    ref = np.zeros_like(par)
+    thr = []
+    rates = oracle.bench_rs8_pinned(10, 4, objs, size, [0, 1, 2, 3], 2, None, 0.02, 0.06,
+                                    parity_out=par, structure=1, throttled=thr)
+    oracle.bench_rs8(0, 10, 4, objs, size, size, n, ref, threads=1)
+    assert len(rates) >= 3 and len(thr) == len(rates)
     assert np.array_equal(par, ref)

@@ -131,3 +131,36 @@ def test_no_cpu_fallback_without_gpu(le):
     assert le.gf_init() == ("error", "No gfx950 HIP device")
     assert le._lib.lib.leoec_host_lanes(None, 0) == le._lib.E_NO_DEVICE
     assert le._lib.lib.leoec_device() == le._lib.E_NO_DEVICE
+
+
+def test_measure_knob_setter_never_writes_the_environment():
+    """The measurement build's knobs are set through leoec_measure_set_knob
+    (an override table inside the library), not setenv: the environment is
+    unchanged, a non-LEOEC name is refused, and a reset drops the overrides.
+    Loaded in a child process (one HIP library per process)."""
+    import subprocess
+    import sys
+    from leo_erasure_amd import _lib
+    if not os.path.exists(_lib.MEASURE_LIB_PATH):
+        pytest.skip("measurement build absent")
+    code = r'''
+import os, sys
+sys.path.insert(0, %r)
+os.environ["LEOEC_LIBRARY"] = "measure"
+from leo_erasure_amd import _lib
+assert _lib.is_measure_build()
+before = dict(os.environ)
+_lib.measure_set_knob("LEOEC_GFBIT_LW", 4)
+_lib.measure_set_knob("LEOEC_GFBIT_LW", None)
+_lib.measure_set_knob("LEOEC_HOST_STAGING", "gather")
+try:
+    _lib.measure_set_knob("PATH", "x")
+    raise SystemExit("non-LEOEC name accepted")
+except ValueError:
+    pass
+_lib.measure_reset_knobs()
+assert dict(os.environ) == before
+print("ok")
+''' % ROOT
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stderr[-2000:]

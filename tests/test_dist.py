@@ -121,6 +121,22 @@ def test_two_ranks_weak_scaling_through_bench_main():
     el = max(r["elapsed_s"] for r in rec["per_rank"])
     assert rec["value"] == pytest.approx(2 * 10 * 65536 * 3 / el / 2**30, rel=2e-2)
     assert all(all(r["checks"].values()) for r in rec["per_rank"])
+    # the whole node's roofline: every rank's bytes over the slowest launch
+    bs = rec["config"]["block_size"]
+    agg = rec["roofline"]["aggregate"]
+    assert agg["n_gpus"] == 2
+    for op, per_obj, key, fkey in (("encode", 14 * bs, "encode_ms", "encode_frac"),
+                                   ("decode", 14 * bs, "decode_ms", "decode_frac")):
+        a = agg[op]
+        slow = max(r[key] for r in rec["per_rank"])
+        assert a["alg_bytes_per_launch"] == 10 * per_obj
+        assert a["slowest_rank_launch_ms"] == pytest.approx(slow, abs=1e-4)
+        assert a["peak"] == 2 * bench.HBM_PEAK_GBS
+        assert a["frac"] == pytest.approx(a["achieved"] / a["peak"], rel=1e-3, abs=6e-5)
+        for r in rec["per_rank"]:  # each rank against one GPU's peak
+            assert r[fkey] == pytest.approx(5 * per_obj / (r[key] * 1e-3) / 1e9 / 8000.0,
+                                            rel=1e-2, abs=6e-5)
+    assert rec["cpu_parity_checked"] is False
 
 
 def test_two_ranks_partitioned_batch():
@@ -151,6 +167,33 @@ def test_single_rank_cpu_leg_checks_parity(monkeypatch):
     cb = rec["cpu_baseline"]
     assert cb["parity_vs_gpu"] == {"objects": 3, "equal": True}
     assert cb["cores"] >= 1 and cb["host_cpus"] >= cb["cores"] and cb["affinity_cpus"] >= 1
+    # one CPU of the share left to the process's other threads
+    assert cb["workers"] == cb["cores"] and cb["cores"] <= max(1, cb["share_cpus"] - 1)
+    assert len(cb["throttled_s_per_pass"]) == len(cb["passes_GiBps"])
+    # the reference's own CPU structure, same sample, same parity check
+    rs = cb["reference_structure"]
+    assert rs["parity_vs_gpu"] == {"objects": 3, "equal": True}
+    assert rs["value"] > 0 and "Jerasure" in rs["structure"] and rs["cores"] == cb["cores"]
+    assert rec["cpu_parity_checked"] is True
+
+
+def test_single_rank_failed_cpu_leg_is_recorded(monkeypatch):
+    """A CPU leg that raises keeps the GPU measurement, and the line says
+    that no CPU-vs-GPU parity check ran."""
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+
+    def boom(*a, **k):
+        raise OSError("no host cores")
+
+    monkeypatch.setattr(bench, "cpu_baseline", boom)
+    argv = ["--objects", "3", "--no-ceiling"] + SMALL
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        rc = bench.main(argv, backend=CpuBackend)
+    rec = json.loads(out.getvalue())
+    assert rc == 0 and rec["cpu_baseline"]["value"] is None
+    assert "no host cores" in rec["cpu_baseline"]["error"]
+    assert rec["cpu_parity_checked"] is False
 
 
 class WithCeiling(CpuBackend):

@@ -32,6 +32,7 @@ struct Geo {
   unsigned ps, bs, nobj, tiles;
   unsigned long long obj;
   unsigned omap;  // 1: xcd_obj_map (the engine's, kernels_impl.hpp)
+  unsigned k;     // input blocks, at run time (the RT forms' loop bound)
 };
 
 __device__ __forceinline__ unsigned obj_map(unsigned b, unsigned n, unsigned tiles) {
@@ -86,7 +87,7 @@ __device__ __forceinline__ void st(const V<LW>& x, __amdgpu_buffer_rsrc_t rs, un
 // (L2-retained) instead of LA, so the neighbouring tile can hit the shared line;
 // EDGE = 2: only the lanes whose bytes lie in the tile's first or last 64 B
 // (the half lines an odd packet shares with the neighbouring tiles) do.
-template <int LW, int WG, int LA, int SA, int EDGE>
+template <int LW, int WG, int LA, int SA, int EDGE, int SB = 0>
 __global__ void __launch_bounds__(WG) pattern(const unsigned char* __restrict__ in,
                                               unsigned char* __restrict__ out, Geo g) {
   constexpr unsigned LB = 4u * LW;
@@ -117,21 +118,143 @@ __global__ void __launch_bounds__(WG) pattern(const unsigned char* __restrict__ 
     }
   };
   load(0, y[0]);
+  if constexpr (SB) {
+    // RT: the engine's shape — a run-time block loop over a 2-slot ring, so
+    // the compiler cannot hoist loads or reassociate the XORs across blocks
+    auto eat = [&](int j, V<LW> (&d)[W]) {
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    if (j + 1 < K) load(j + 1, y[(j + 1) & 1]);
+      for (int i = 0; i < R; ++i)
 #pragma unroll
-    for (int i = 0; i < R; ++i)
+        for (int x = 0; x < W; ++x)
 #pragma unroll
-      for (int x = 0; x < W; ++x)
+          for (int e = 0; e < LW; ++e) acc[i][x].v[e] ^= d[x].v[e] + (unsigned)(i * 3 + j);
+    };
+    const int kk = (int)g.k;
+#pragma unroll 1
+    for (int j = 0; j < kk; j += 2) {
+      if (j + 1 < kk) load(j + 1, y[1]);
+      eat(j, y[0]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (j + 1 >= kk) break;
+      if (j + 2 < kk) load(j + 2, y[0]);
+      eat(j + 1, y[1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
 #pragma unroll
-        for (int e = 0; e < LW; ++e) acc[i][x].v[e] ^= y[j & 1][x].v[e] + (unsigned)(i * 3 + j);
+    for (int j = 0; j < K; ++j) {
+      if (j + 1 < K) load(j + 1, y[(j + 1) & 1]);
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int x = 0; x < W; ++x)
+#pragma unroll
+          for (int e = 0; e < LW; ++e) acc[i][x].v[e] ^= y[j & 1][x].v[e] + (unsigned)(i * 3 + j);
+    }
   }
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const auto rs = rsrc(ob + (size_t)i * g.bs, g.bs);
 #pragma unroll
     for (int x = 0; x < W; ++x) st<LW, SA>(acc[i][x], rs, x * g.ps + off);
+  }
+}
+
+// The 8-byte-column register layout of `pattern<2, ...>` (the shipped LW = 2:
+// acc 64 VGPRs, ring 32) fed by 16-byte memory instructions.  For packet
+// pair (2p, 2p+1) lanes 0-31 of a wave load 16 B of packet 2p and lanes
+// 32-63 16 B of packet 2p+1, over the same 512-B span; two
+// v_permlane32_swap_b32 per pair (dwords 0<->2, 1<->3, lanes 32-63 of the
+// first with lanes 0-31 of the second) then leave lane l holding one 8-byte
+// column of BOTH packets: lane l < 32 column 2l, lane l + 32 column 2l + 1.
+// Raw loads stay in the ring until the block is consumed (a swap at load
+// time would wait on the load).  Stores: the same swaps (an involution),
+// then one 16-byte store per pair.  Lanes past the packet load from an
+// out-of-range offset (the buffer returns zeros) and do not store.
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void swap_pair(unsigned& a, unsigned& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+  a = r[0];
+  b = r[1];
+}
+
+template <int WG, int LA, int SA, int SB = 0>
+__global__ void __launch_bounds__(WG) pattern_swap(const unsigned char* __restrict__ in,
+                                                   unsigned char* __restrict__ out, Geo g) {
+  static_assert(W % 2 == 0, "packet pairs");
+  const unsigned b = g.omap ? obj_map(blockIdx.x, gridDim.x, g.tiles) : blockIdx.x;
+  const unsigned obj = b / g.tiles, tile = b % g.tiles;
+  const unsigned lane = threadIdx.x & 63u, half = lane >> 5;
+  const unsigned wbase = tile * (WG * 8u) + (threadIdx.x >> 6) * 512u;
+  if (wbase >= g.ps) return;  // whole wave past the packet
+  const unsigned off = wbase + (lane & 31u) * 16u;
+  const bool live = off < g.ps;
+  const unsigned char* ib = in + (size_t)obj * g.obj;
+  unsigned char* ob = out + (size_t)obj * R * g.bs;
+  unsigned acc[R][W][2];
+  for (int i = 0; i < R; ++i)
+    for (int x = 0; x < W; ++x) acc[i][x][0] = acc[i][x][1] = 0u;
+  u4v raw[2][W / 2];
+  auto load = [&](int j, u4v (&d)[W / 2]) {
+    const auto rs = rsrc(ib + (size_t)j * g.bs, g.bs);
+#pragma unroll
+    for (int p = 0; p < W / 2; ++p)
+      d[p] = __builtin_amdgcn_raw_buffer_load_b128(
+          rs, live ? (2u * p + half) * g.ps + off : 0x80000000u, 0, LA);
+  };
+  auto eat = [&](int j, const u4v (&d)[W / 2]) {
+    unsigned y[W][2];
+#pragma unroll
+    for (int p = 0; p < W / 2; ++p) {
+      u4v v = d[p];
+      unsigned a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
+      swap_pair(a0, a2);
+      swap_pair(a1, a3);
+      y[2 * p][0] = a0;
+      y[2 * p][1] = a1;
+      y[2 * p + 1][0] = a2;
+      y[2 * p + 1][1] = a3;
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int x = 0; x < W; ++x)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) acc[i][x][e] ^= y[x][e] + (unsigned)(i * 3 + j);
+  };
+  load(0, raw[0]);
+  if constexpr (SB) {  // RT: as pattern<..., SB = 1>
+    const int kk = (int)g.k;
+#pragma unroll 1
+    for (int j = 0; j < kk; j += 2) {
+      if (j + 1 < kk) load(j + 1, raw[1]);
+      eat(j, raw[0]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (j + 1 >= kk) break;
+      if (j + 2 < kk) load(j + 2, raw[0]);
+      eat(j + 1, raw[1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (j + 1 < K) load(j + 1, raw[(j + 1) & 1]);
+      eat(j, raw[j & 1]);
+    }
+  }
+  if (!live) return;  // after the last swap: every lane took part in it
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const auto rs = rsrc(ob + (size_t)i * g.bs, g.bs);
+#pragma unroll
+    for (int p = 0; p < W / 2; ++p) {
+      unsigned a0 = acc[i][2 * p][0], a1 = acc[i][2 * p][1];
+      unsigned a2 = acc[i][2 * p + 1][0], a3 = acc[i][2 * p + 1][1];
+      swap_pair(a0, a2);
+      swap_pair(a1, a3);
+      __builtin_amdgcn_raw_buffer_store_b128(u4v{a0, a1, a2, a3}, rs, (2u * p + half) * g.ps + off,
+                                             0, SA);
+    }
   }
 }
 
@@ -151,6 +274,9 @@ struct Case {
   unsigned wg, lb, omap;
 };
 #define KC(LW, WG, LA, SA, E) reinterpret_cast<KFn>(&pattern<LW, WG, LA, SA, (int)(E)>)
+#define KS(WG, LA, SA) reinterpret_cast<KFn>(&pattern_swap<WG, LA, SA>)
+#define KSB(WG) reinterpret_cast<KFn>(&pattern_swap<WG, 2, 2, 1>)
+#define KCB(LW, WG) reinterpret_cast<KFn>(&pattern<LW, WG, 2, 2, 0, 1>)
 
 int main(int argc, char** argv) {
   const unsigned nobj = argc > 1 ? (unsigned)atoi(argv[1]) : 1024u;
@@ -162,6 +288,7 @@ int main(int argc, char** argv) {
   G.ps = G.bs / W;
   G.obj = osz;
   G.nobj = nobj;
+  G.k = K;
   printf("# object %llu B, bs %u, ps %u (ps mod 128 = %u), %u objects\n", osz, G.bs, G.ps,
          G.ps % 128, nobj);
   unsigned char *in, *out;
@@ -173,9 +300,39 @@ int main(int argc, char** argv) {
   CHECK(hipMemset(out, 0, out_bytes));
   CHECK(hipDeviceSynchronize());
   const double bytes = (double)nobj * (K + R) * G.bs;
+  {
+    // the swap forms must produce the 8-byte-lane forms' output exactly (same
+    // dword arithmetic, columns only permuted over lanes): one launch each,
+    // outputs compared byte for byte
+    std::vector<unsigned char> ref(out_bytes), got(out_bytes);
+    Geo g = G;
+    g.omap = 1;
+    g.tiles = (G.ps + 2047u) / 2048u;
+    auto run = [&](KFn k, std::vector<unsigned char>& dst) {
+      CHECK(hipMemset(out, 0, out_bytes));
+      hipLaunchKernelGGL(k, dim3(nobj * g.tiles), dim3(256), 0, 0, in, out, g);
+      CHECK(hipMemcpy(dst.data(), out, out_bytes, hipMemcpyDeviceToHost));
+    };
+    const KFn pairs[2][2] = {{KC(2, 256, 2, 2, 0), KS(256, 2, 2)}, {KCB(2, 256), KSB(256)}};
+    for (int q = 0; q < 2; ++q) {
+      run(pairs[q][0], ref);
+      run(pairs[q][1], got);
+      size_t bad = 0;
+      for (size_t i = 0; i < out_bytes; ++i) bad += ref[i] != got[i];
+      printf("# swap form vs 8-byte-lane form (%s): %zu of %zu output bytes differ\n",
+             q ? "run-time K ring" : "unrolled", bad, out_bytes);
+      if (bad) return 3;
+    }
+  }
   std::vector<Case> cases = {
-      {"lw8 wg256 nt/nt", KC(2, 256, 2, 2, false), 256, 8, 0},
-      {"lw8 wg256 nt/nt objmap", KC(2, 256, 2, 2, false), 256, 8, 1},
+      {"lw8 wg256 nt/nt objmap (shipped shape)", KC(2, 256, 2, 2, false), 256, 8, 1},
+      {"swap16 wg256 nt/nt objmap", KS(256, 2, 2), 256, 8, 1},
+      {"swap16 wg128 nt/nt objmap", KS(128, 2, 2), 128, 8, 1},
+      {"swap16 wg512 nt/nt objmap", KS(512, 2, 2), 512, 8, 1},
+      {"swap16 wg256 nt/nt", KS(256, 2, 2), 256, 8, 0},
+      {"lw8 wg256 nt/nt objmap ring (run-time K ring)", KCB(2, 256), 256, 8, 1},
+      {"swap16 wg256 nt/nt objmap ring (run-time K ring)", KSB(256), 256, 8, 1},
+      {"swap16 wg128 nt/nt objmap ring (run-time K ring)", KSB(128), 128, 8, 1},
       {"lw8 wg256 nt/nt objmap edge-waves-L2", KC(2, 256, 2, 2, true), 256, 8, 1},
       {"lw8 wg256 ld0/nt objmap", KC(2, 256, 0, 2, false), 256, 8, 1},
       {"lw8 wg256 sc1nt/nt objmap", KC(2, 256, 18, 2, false), 256, 8, 1},
