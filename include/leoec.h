@@ -150,14 +150,24 @@ int leoec_coding_matrix(int coding, int k, int m, int w, uint32_t *out, int cap,
  * or a negative status. */
 int leoec_device(void);
 
-/* Host-memory calls (leoec_encode / _decode / _repair) are spread over the
- * node's gfx950 devices: each call goes to the dispatcher lane with the
- * fewest calls in progress (one lane per device, each with its own batching
- * queue and PCIe link); the caller's current device is left as it was.
- * Returns the number of lanes and writes the device ordinal of lane i to
+/* Host-memory calls (leoec_encode / _decode / _repair) run on the calling
+ * thread's current HIP device by default (each device has its own batching
+ * queue, its dispatcher lane).  Returns the number of lanes (one per gfx950
+ * device visible to the process) and writes the device ordinal of lane i to
  * devices[i] for i < cap (devices may be NULL), or a negative status.
  * (No reference counterpart: the reference is CPU-only.) */
 int leoec_host_lanes(int *devices, int cap);
+
+/* Opt in to spreading host-memory calls over several devices: with n > 0,
+ * each later call goes to the device of devices[0..n-1] whose lane has the
+ * fewest calls in progress (its own queue and PCIe link), and the caller's
+ * current device is left as it was; n == 0 restores the default (the
+ * caller's current device).  Every ordinal must be a gfx950 device visible
+ * to the process (else LEOEC_E_NO_DEVICE, and the setting is unchanged).
+ * Returns the number of devices in the set.  Only the devices used get
+ * queues and pinned arenas (5 x 32 MiB pinned + 5 x 32 MiB device each).
+ * (No reference counterpart: the reference is CPU-only.) */
+int leoec_host_spread(const int *devices, int n);
 
 /* Library version string. */
 const char *leoec_version(void);

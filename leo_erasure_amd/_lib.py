@@ -35,7 +35,8 @@ E_HIP = -17
 EXPORTS = (
     "leoec_strerror", "leoec_gf_init", "leoec_check_params", "leoec_layout", "leoec_encode",
     "leoec_decode", "leoec_repair", "leoec_encode_dev", "leoec_decode_dev", "leoec_repair_dev",
-    "leoec_coding_matrix", "leoec_device", "leoec_host_lanes", "leoec_version",
+    "leoec_coding_matrix", "leoec_device", "leoec_host_lanes", "leoec_host_spread",
+    "leoec_version",
 )
 
 
@@ -67,6 +68,8 @@ def _load(path=LIB_PATH):
     L.leoec_device.argtypes = []
     if hasattr(L, "leoec_host_lanes"):  # (absent from pre-round-3 builds, A/B tools)
         L.leoec_host_lanes.argtypes = [ctypes.POINTER(c_int), c_int]
+    if hasattr(L, "leoec_host_spread"):  # (absent from pre-round-4 builds)
+        L.leoec_host_spread.argtypes = [ctypes.POINTER(c_int), c_int]
     L.leoec_check_params.argtypes = [c_int] * 4
     L.leoec_layout.argtypes = [c_int] * 4 + [u64, ctypes.POINTER(u64), ctypes.POINTER(c_int)]
     L.leoec_encode.argtypes = [c_int] * 4 + [u8p, u64, u8p, u64]
@@ -180,8 +183,18 @@ def version():
     return lib.leoec_version().decode()
 
 
+def host_spread(devices):
+    """Spread host-memory calls over these device ordinals ([] restores the
+    default: each call on the caller's current device); returns the count."""
+    arr = (ctypes.c_int * max(len(devices), 1))(*devices)
+    n = lib.leoec_host_spread(arr, len(devices))
+    if n < 0:
+        raise LeoecError(n)
+    return n
+
+
 def host_lanes():
-    """Device ordinal of each lane the host-memory calls are spread over."""
+    """Device ordinal of each dispatcher lane (one per gfx950 device)."""
     n = lib.leoec_host_lanes(None, 0)
     if n < 0:
         raise LeoecError(n)

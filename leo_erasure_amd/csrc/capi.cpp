@@ -158,6 +158,10 @@ int leoec_host_lanes(int* devices, int cap) {
   });
 }
 
+int leoec_host_spread(const int* devices, int n) {
+  return guarded([&] { return leoec::hostq_spread(devices, n); });
+}
+
 const char* leoec_version(void) { return LEOEC_VERSION " (gfx950)"; }
 
 }  // extern "C"

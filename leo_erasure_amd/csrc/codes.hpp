@@ -11,6 +11,7 @@
 // jerasure_schedule_decode_*_lazy and IRSCoding::gf_gen_decode_matrix.
 #pragma once
 
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 

@@ -269,16 +269,37 @@ int build_plan(const Code& c, const int* surv, const int* want, int nwant, Plan*
 }
 
 // Plans by (code, knobs that pick a kernel family, survivors, wanted ids).
-// Bounded: past kPlanCacheMax entries the cache starts over (plans in use
-// live on through their shared_ptr).
+// Bounded by entries and by bytes: past kPlanCacheMax entries or
+// kPlanCacheBytes of plan tables the cache starts over (plans in use live on
+// through their shared_ptr), and a plan larger than kPlanCacheOne (a
+// generic-bitmatrix plan of a large k at w = 32 keeps one byte per bit,
+// nwant*w x k*w) is built per call and never cached, so distinct erasure
+// patterns cannot pin more than kPlanCacheBytes of host memory.
+// (LEOEC_PLAN_CACHE_BYTES / _ONE: smaller bounds for the host sanitizer
+// harness, tests/host_sanitize, so its churn crosses them)
+#ifndef LEOEC_PLAN_CACHE_BYTES
+#define LEOEC_PLAN_CACHE_BYTES ((size_t)64 << 20)
+#endif
+#ifndef LEOEC_PLAN_CACHE_ONE
+#define LEOEC_PLAN_CACHE_ONE ((size_t)4 << 20)
+#endif
 constexpr size_t kPlanCacheMax = 4096;
+constexpr size_t kPlanCacheBytes = LEOEC_PLAN_CACHE_BYTES;
+constexpr size_t kPlanCacheOne = LEOEC_PLAN_CACHE_ONE;
 
 }  // namespace
+
+size_t plan_bytes(const Plan& p) {
+  return sizeof(Plan) + p.coef.size() * sizeof(uint32_t) + p.bits.size() +
+         p.mbits.size() * sizeof(uint32_t) + p.lib_pos.size() * sizeof(int) +
+         (p.surv.size() + p.want.size()) * sizeof(int);
+}
 
 int make_plan(const Code& c, const int* surv, const int* want, int nwant,
               std::shared_ptr<const Plan>* out) {
   static std::mutex mu;
   static std::map<std::vector<intptr_t>, std::shared_ptr<const Plan>> cache;
+  static size_t cached_bytes = 0;
   std::vector<intptr_t> key;
   key.reserve(4 + c.k + nwant);
   key.push_back((intptr_t)&c);
@@ -298,9 +319,19 @@ int make_plan(const Code& c, const int* surv, const int* want, int nwant,
   auto p = std::make_shared<Plan>();
   const int rc = build_plan(c, surv, want, nwant, p.get());  // outside the lock
   if (rc) return rc;
+  const size_t nb = plan_bytes(*p);
+  if (nb > kPlanCacheOne) {  // too large to keep: this call's own
+    *out = std::move(p);
+    return LEOEC_OK;
+  }
   std::lock_guard<std::mutex> lock(mu);
-  if (cache.size() >= kPlanCacheMax) cache.clear();
-  *out = cache.emplace(std::move(key), std::move(p)).first->second;
+  if (cache.size() >= kPlanCacheMax || cached_bytes + nb > kPlanCacheBytes) {
+    cache.clear();
+    cached_bytes = 0;
+  }
+  auto ins = cache.emplace(std::move(key), std::move(p));
+  if (ins.second) cached_bytes += nb;
+  *out = ins.first->second;
   return LEOEC_OK;
 }
 
@@ -743,7 +774,9 @@ int stage_d2h_sync(Staging* st, const std::vector<D2HSeg>& segs) {
   return hip_ok(hipStreamSynchronize(st->stream));
 }
 
-int get_staging(size_t bytes, Staging** out) {
+// This thread's staging on its current device (stream only: the buffers
+// come from zc_ready or dev_buf, whichever form the call takes).
+int get_staging(Staging** out) {
   int rc = device_init();
   if (rc) return rc;
   int dev = 0;
@@ -755,18 +788,35 @@ int get_staging(size_t bytes, Staging** out) {
       return LEOEC_E_HIP;
     st.device = dev;
   }
-  if (st.cap < bytes) {
-    if (st.buf) {
-      (void)hipStreamSynchronize(st.stream);
-      (void)hipFree(st.buf);
-      st.buf = nullptr;
-      st.cap = 0;
-    }
-    const size_t want = std::max<size_t>(bytes + bytes / 4, (size_t)1 << 20);
-    if (hipMalloc(&st.buf, want) != hipSuccess) return LEOEC_E_NOMEM;
-    st.cap = want;
-  }
   *out = &st;
+  return LEOEC_OK;
+}
+
+// The device buffer of the copy forms, grown to `bytes` (the zero-copy form
+// never allocates one: round 3's advisor found every call paying for it).
+int dev_buf(Staging* st, size_t bytes) {
+  if (st->cap >= bytes) return LEOEC_OK;
+  if (st->buf) {
+    (void)hipStreamSynchronize(st->stream);
+    (void)hipFree(st->buf);
+    st->buf = nullptr;
+    st->cap = 0;
+  }
+  const size_t want = std::max<size_t>(bytes + bytes / 4, (size_t)1 << 20);
+  if (hipMalloc(&st->buf, want) != hipSuccess) return LEOEC_E_NOMEM;
+  st->cap = want;
+  return LEOEC_OK;
+}
+
+// Staging for a call moving `bytes`: the zero-copy form when it applies,
+// else the copy forms' device buffer.
+int stage_for(size_t bytes, Staging** out, bool* zc) {
+  Staging* st;
+  int rc = get_staging(&st);
+  if (rc) return rc;
+  *zc = zc_ready(st, bytes);
+  if (!*zc && (rc = dev_buf(st, bytes))) return rc;
+  *out = st;
   return LEOEC_OK;
 }
 
@@ -811,9 +861,9 @@ int run_host_map(const Plan& plan, const uint8_t* const* blocks, const std::vect
   if (c.bitmatrix && (bs % (16ull * (uint64_t)c.w))) return LEOEC_E_BAD_SIZE;
   Staging* st;
   const size_t span = (size_t)(k + want.size()) * bs16;
-  int rc = get_staging(span, &st);
+  bool zc;
+  int rc = stage_for(span, &st, &zc);
   if (rc) return rc;
-  const bool zc = zc_ready(st, span);
   uint8_t* base = zc ? st->zd : st->buf;
   std::vector<Shard> in(k), out(want.size());
   std::vector<H2DSeg> segs(k);
@@ -920,9 +970,9 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
   DeviceScope on(ticket.device);  // the per-thread path, on the device the dispatcher picked
   if (!on.ok()) return LEOEC_E_HIP;
   Staging* st;
-  rc = get_staging((size_t)(k + m) * bs, &st);
+  bool zc;
+  rc = stage_for((size_t)(k + m) * bs, &st, &zc);
   if (rc) return rc;
-  const bool zc = zc_ready(st, (size_t)(k + m) * bs);
   uint8_t* base = zc ? st->zd : st->buf;
   std::vector<Shard> in(k), par(m);
   for (int j = 0; j < k; ++j)

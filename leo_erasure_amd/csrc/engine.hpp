@@ -51,6 +51,8 @@ struct Plan {
 // their inverse.  The shared_ptr keeps a plan alive while a batch uses it.
 int make_plan(const Code& c, const int* surv, const int* want, int nwant,
               std::shared_ptr<const Plan>* out);
+// Host bytes a plan holds (its tables): the plan cache's size bound.
+size_t plan_bytes(const Plan& p);
 // Enqueue a plan over a batch.  in: k shards in survivor order; out: nwant.
 int run_plan(const Plan& p, const std::vector<Shard>& in, const std::vector<Shard>& out,
              uint64_t block_size, uint64_t nobj, hipStream_t s);

@@ -301,17 +301,23 @@ void completer_main(Queue* q) {
   }
 }
 
-// Dispatcher lanes: lane i runs on host_devices()[i % ndev].  The product
-// has one lane per gfx950 device; the measurement knob LEOEC_HOSTQ_LANES
-// maps more lanes onto fewer devices (the dispatcher's test on a one-GPU
-// box).  Each lane has a queue, created on first use; its two threads live
-// for the process (they hold no GPU work when idle, and a process exits with
-// them parked on their condition variables; libleoec.so is linked
-// -z nodelete so their code is never unmapped).
+// Dispatcher lanes: lane i runs on host_devices()[i % ndev], one lane per
+// gfx950 device.  By default a host-memory call runs on the lane of the
+// caller's current device (the reference NIF's contract: the library uses
+// what the process was given, and one process per GPU stays on its GPU);
+// leoec_host_spread() opts in to spreading calls over a set of devices, each
+// call going to the lane with the fewest calls in progress.  The measurement
+// knob LEOEC_HOSTQ_LANES maps more lanes onto fewer devices and spreads over
+// all of them (the dispatcher's test on a one-GPU box).  Each lane has a
+// queue, created on first use; its two threads live for the process (they
+// hold no GPU work when idle, and a process exits with them parked on their
+// condition variables; libleoec.so is linked -z nodelete so their code is
+// never unmapped).
 constexpr int kMaxLanes = 64;
 
 std::atomic<int> g_load[kMaxLanes];  // calls in progress per lane
 std::atomic<unsigned> g_rr{0};
+std::atomic<uint64_t> g_spread{0};   // lanes host calls spread over; 0: the caller's device
 
 int lane_count() {
   const int ndev = (int)host_devices().size();
@@ -324,21 +330,47 @@ int lane_device(int lane) {
   return d[(size_t)lane % d.size()];
 }
 
-// The lane with the fewest calls in progress, ties broken round-robin.
-int pick_lane() {
+// The lane in `mask` with the fewest calls in progress, ties broken
+// round-robin.
+int least_loaded(uint64_t mask) {
   const int n = lane_count();
   const unsigned start = g_rr.fetch_add(1, std::memory_order_relaxed);
-  int best = (int)(start % (unsigned)n);
-  int best_load = g_load[best].load(std::memory_order_relaxed);
-  for (int i = 1; i < n && best_load > 0; ++i) {
+  int best = -1, best_load = 0;
+  for (int i = 0; i < n; ++i) {
     const int l = (int)((start + (unsigned)i) % (unsigned)n);
+    if (!((mask >> l) & 1u)) continue;
     const int x = g_load[l].load(std::memory_order_relaxed);
-    if (x < best_load) {
+    if (best < 0 || x < best_load) {
       best = l;
       best_load = x;
+      if (x == 0) break;
     }
   }
   return best;
+}
+
+// The lane for this call: see above.  LEOEC_E_NO_DEVICE when the caller's
+// current device is not one of the gfx950 devices.
+int pick_lane(int* lane) {
+  if (knobs().hostq_lanes > 0) {
+    const int n = lane_count();
+    *lane = least_loaded(n >= 64 ? ~0ull : ((1ull << n) - 1));
+    return LEOEC_OK;
+  }
+  const uint64_t spread = g_spread.load(std::memory_order_acquire);
+  if (spread) {
+    *lane = least_loaded(spread);
+    return *lane >= 0 ? LEOEC_OK : LEOEC_E_NO_DEVICE;
+  }
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return LEOEC_E_HIP;
+  const std::vector<int>& d = host_devices();
+  for (size_t i = 0; i < d.size(); ++i)
+    if (d[i] == dev) {
+      *lane = (int)i;
+      return LEOEC_OK;
+    }
+  return LEOEC_E_NO_DEVICE;
 }
 
 Queue* queue_for(int lane) {
@@ -387,10 +419,29 @@ HostqTicket::~HostqTicket() {
 
 int hostq_lanes() { return device_init() == LEOEC_OK ? lane_count() : 0; }
 
+int hostq_spread(const int* devices, int n) {
+  int rc = device_init();
+  if (rc) return rc;
+  if (n < 0 || (n > 0 && !devices)) return LEOEC_E_ARG;
+  const std::vector<int>& d = host_devices();
+  uint64_t mask = 0;
+  for (int i = 0; i < n; ++i) {
+    size_t j = 0;
+    while (j < d.size() && d[j] != devices[i]) ++j;
+    if (j == d.size()) return LEOEC_E_NO_DEVICE;  // not a gfx950 device of this process
+    mask |= 1ull << j;
+  }
+  g_spread.store(mask, std::memory_order_release);
+  int lanes = 0;
+  for (uint64_t x = mask; x; x &= x - 1) ++lanes;
+  return lanes;
+}
+
 int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), void* arg) {
   int rc = device_init();
   if (rc) return rc;
-  const int lane = pick_lane();
+  int lane = -1;
+  if ((rc = pick_lane(&lane))) return rc;
   g_load[lane].fetch_add(1, std::memory_order_relaxed);
   ticket->lane = lane;  // charged until the call returns (~HostqTicket)
   ticket->device = lane_device(lane);

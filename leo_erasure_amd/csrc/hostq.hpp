@@ -64,11 +64,11 @@ struct HostqTicket {
   ~HostqTicket();
 };
 
-// Run `job` on one of the node's gfx950 devices and wait for it.  The
-// dispatcher gives each call the lane (one queue per device; the
-// measurement build can map more lanes onto fewer devices) with the fewest
-// calls in progress, ties taken round-robin, so concurrent callers spread
-// over every device and its PCIe link.  `overlap` (may be null) runs on the
+// Run `job` and wait for it: on the caller's current device by default, or,
+// after hostq_spread(), on the lane (one queue per device; the measurement
+// build can map more lanes onto fewer devices) of the spread set with the
+// fewest calls in progress, ties taken round-robin, so concurrent callers
+// spread over those devices and their PCIe links.  `overlap` (may be null) runs on the
 // caller's thread while the batch is on the GPU.  Returns a leoec_status
 // (this job's own: another caller's failed launch does not fail it), or
 // kNotBatched: nothing was done and the caller runs its per-thread path on
@@ -79,8 +79,13 @@ constexpr int kNotBatched = 1;
 int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*) = nullptr,
               void* arg = nullptr);
 
-// Dispatcher lanes in use (one per gfx950 device in the product build), or
-// 0 without a device.
+// Dispatcher lanes (one per gfx950 device in the product build), or 0
+// without a device.
 int hostq_lanes();
+
+// leoec_host_spread: spread host-memory calls over these device ordinals
+// (n > 0), or run each on the caller's current device again (n == 0).
+// Returns the number of lanes in the set or a negative status.
+int hostq_spread(const int* devices, int n);
 
 }  // namespace leoec

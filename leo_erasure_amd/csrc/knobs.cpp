@@ -5,9 +5,11 @@
 #include <atomic>
 #include <cstdlib>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <string_view>
+#include <vector>
 #endif
 
 namespace leoec {
@@ -43,8 +45,16 @@ int env_int(const char* name, int dflt) {
   return e ? std::atoi(e) : dflt;
 }
 
+// Every snapshot ever published, kept (reachable) for the process: a
+// launch may still read an older one.  Guarded by g_mu.
+std::vector<std::unique_ptr<const Knobs>>& snapshots() {
+  static auto* v = new std::vector<std::unique_ptr<const Knobs>>;
+  return *v;
+}
+
 const Knobs* read_env() {
   Knobs* k = new Knobs;
+  snapshots().emplace_back(k);
   k->bitmatrix = env_int("LEOEC_BITMATRIX", k->bitmatrix);
   if (const char* e = lookup("LEOEC_HOST_STAGING")) {
     const std::string_view v(e);

@@ -1,0 +1,258 @@
+// Host-side stress test of the engine's C ABI under the sanitizers, TEST
+// INFRASTRUCTURE ONLY (tests/test_host_sanitize.py builds it with the fake
+// HIP runtime of this directory, once with -fsanitize=address,undefined and
+// once with -fsanitize=thread).
+//
+// What runs: the plan cache (engine.cpp make_plan), the per-thread staging
+// (engine.cpp Staging, zero-copy / copy forms), the batching queue
+// (hostq.cpp: slots, worker, completer, per-job status) and the dispatcher
+// lanes (default: the caller's device; leoec_host_spread), driven by many
+// concurrent callers as the reference's NIF is (basho_bench {concurrent, 4},
+// test/basho_bench_leo_erasure_rs_10_4_8_1M_w_t4.config:24;
+// c_src/leo_erasure_nif.cpp:346-351).  Every result is compared with the CPU
+// oracle (oracle/leoec_oracle.c).  In the measurement build
+// (-DLEOEC_MEASURE) one more thread flips staging / queue knobs through
+// leoec_measure_set_knob while the callers run.
+//
+//   host_stress [threads] [rounds]     exit 0 = every result bit-exact
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include <hip/hip_runtime.h>  // the fake runtime of this directory (hipSetDevice)
+
+#include "../../include/leoec.h"
+extern "C" {
+#include "../../oracle/leoec_oracle.h"
+}
+
+#ifdef LEOEC_MEASURE
+extern "C" int leoec_measure_set_knob(const char* name, const char* value);
+extern "C" void leoec_measure_reset_knobs(void);
+#endif
+
+namespace {
+
+struct Case {
+  int coding, k, m, w;
+  uint64_t size;
+  std::vector<uint8_t> data, ref;  // ref: the oracle's (k+m)*bs blocks
+  uint64_t bs = 0;
+  int filled = 0;
+};
+
+std::mutex g_err_mu;
+std::vector<std::string> g_errs;
+void fail(const std::string& e) {
+  std::lock_guard<std::mutex> l(g_err_mu);
+  if (g_errs.size() < 20) g_errs.push_back(e);
+}
+
+std::string name(const Case& c) {
+  char b[96];
+  std::snprintf(b, sizeof b, "coding %d (%d,%d,%d) size %llu", c.coding, c.k, c.m, c.w,
+                (unsigned long long)c.size);
+  return b;
+}
+
+void prepare(Case* c, uint32_t seed) {
+  std::mt19937 rng(seed);
+  c->data.resize(c->size);
+  for (auto& x : c->data) x = (uint8_t)rng();
+  c->bs = orc_block_size(c->k, c->w, c->size);
+  c->ref.assign((size_t)(c->k + c->m) * c->bs, 0);
+  if (orc_encode(c->coding, c->k, c->m, c->w, c->data.data(), c->size, c->ref.data()))
+    std::abort();
+  uint64_t bs = 0;
+  if (leoec_layout(c->coding, c->k, c->m, c->w, c->size, &bs, &c->filled) || bs != c->bs)
+    std::abort();
+}
+
+const uint8_t* block(const Case& c, int id) { return c.ref.data() + (size_t)id * c.bs; }
+
+// encode, decode (m blocks lost, survivors listed in reverse), repair of two
+// blocks; t picks the erasure pattern
+void roundtrip(const Case& c, int t) {
+  const int k = c.k, m = c.m, n = k + m;
+  const uint64_t bs = c.bs;
+  {
+    std::vector<uint8_t> out((size_t)(n - c.filled) * bs + 1);
+    const int rc = leoec_encode(c.coding, k, m, c.w, c.data.data(), c.size, out.data(), out.size());
+    if (rc || std::memcmp(out.data(), block(c, c.filled), (size_t)(n - c.filled) * bs))
+      fail("encode " + name(c) + " rc " + std::to_string(rc));
+  }
+  std::vector<int> lost, ids;
+  for (int j = 0; j < m; ++j) {
+    const int id = (t * 7 + j * 3) % n;
+    bool dup = false;
+    for (int x : lost) dup |= x == id;
+    if (!dup) lost.push_back(id);
+  }
+  for (int id = n - 1; id >= 0; --id) {
+    bool gone = false;
+    for (int x : lost) gone |= x == id;
+    if (!gone) ids.push_back(id);
+  }
+  {
+    std::vector<const uint8_t*> ptrs;
+    for (int id : ids) ptrs.push_back(block(c, id));
+    std::vector<uint8_t> out(c.size + 1);
+    const int rc = leoec_decode(c.coding, k, m, c.w, ptrs.data(), ids.data(), (int)ids.size(), bs,
+                                c.size, out.data());
+    if (rc || std::memcmp(out.data(), c.data.data(), c.size))
+      fail("decode " + name(c) + " rc " + std::to_string(rc));
+  }
+  {
+    const int rep[2] = {t % n, (t + 5) % n};
+    const int nrep = rep[0] == rep[1] ? 1 : 2;
+    std::vector<int> avail;
+    std::vector<const uint8_t*> ptrs;
+    for (int id = 0; id < n; ++id)
+      if (id != rep[0] && id != rep[1]) {
+        avail.push_back(id);
+        ptrs.push_back(block(c, id));
+      }
+    std::vector<uint8_t> out((size_t)nrep * bs + 1);
+    const int rc = leoec_repair(c.coding, k, m, c.w, ptrs.data(), avail.data(), (int)avail.size(),
+                                bs, rep, nrep, out.data());
+    bool ok = rc == 0;
+    for (int r = 0; ok && r < nrep; ++r)
+      ok = !std::memcmp(out.data() + (size_t)r * bs, block(c, rep[r]), bs);
+    if (!ok) fail("repair " + name(c) + " rc " + std::to_string(rc));
+  }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const int threads = argc > 1 ? std::atoi(argv[1]) : 16;
+  const int rounds = argc > 2 ? std::atoi(argv[2]) : 6;
+  if (leoec_gf_init() != LEOEC_OK) {
+    std::fprintf(stderr, "gf_init failed\n");
+    return 2;
+  }
+  // the engine's batching and staging thresholds: objects around kGatherMax
+  // and kBatchMaxJobBytes (8 / 16 MiB) would make the CPU kernels slow, so
+  // the shapes cover the code paths at small sizes plus one 9 MiB object
+  std::vector<Case> cases = {
+      {LEOEC_VANDRS, 10, 4, 8, 262144},   {LEOEC_VANDRS, 10, 4, 8, 100003},
+      {LEOEC_CAUCHYRS, 10, 4, 8, 80077},  {LEOEC_ISARS, 10, 4, 8, 65543},
+      {LEOEC_LIBERATION, 4, 2, 7, 77777}, {LEOEC_VANDRS, 4, 2, 16, 23457},
+      {LEOEC_VANDRS, 6, 3, 32, 9999},     {LEOEC_CAUCHYRS, 4, 2, 3, 5000},
+      {LEOEC_VANDRS, 20, 6, 8, 200003},   {LEOEC_CAUCHYRS, 5, 3, 17, 40000},
+      {LEOEC_LIBERATION, 5, 2, 5, 3001},
+  };
+  Case big{LEOEC_VANDRS, 10, 4, 8, (9u << 20) + 5};  // per-thread path (> the batch cap)
+  for (size_t i = 0; i < cases.size(); ++i) prepare(&cases[i], 100 + (uint32_t)i);
+  prepare(&big, 99);
+
+  // phase 1: concurrent callers on the default lane (the caller's device);
+  // half the threads on device 1
+  auto phase = [&](const char* what, bool spread_devices) {
+    std::atomic<bool> stop{false};
+#ifdef LEOEC_MEASURE
+    std::thread flipper([&] {
+      const char* staging[] = {"auto", "gather", "pageable", "pinned", "zerocopy"};
+      const char* direct[] = {"0", "4"};
+      unsigned i = 0;
+      while (!stop.load()) {
+        leoec_measure_set_knob("LEOEC_HOST_STAGING", staging[i % 5]);
+        leoec_measure_set_knob("LEOEC_HOSTQ_DIRECT", direct[i % 2]);
+        leoec_measure_set_knob("LEOEC_HOSTQ_DIRECT_MAP", direct[(i / 2) % 2]);
+        leoec_measure_set_knob("LEOEC_STAGE_CHUNK_KIB", i % 3 ? "16" : "256");
+        ++i;
+        std::this_thread::sleep_for(std::chrono::milliseconds(3));
+      }
+      leoec_measure_reset_knobs();
+    });
+#endif
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+      th.emplace_back([&, t] {
+        if (!spread_devices && (t & 1)) hipSetDevice(1);
+        for (int r = 0; r < rounds; ++r) roundtrip(cases[(size_t)(t + r) % cases.size()], t + r);
+        if (t == 0) roundtrip(big, 3);
+      });
+    for (auto& x : th) x.join();
+    stop = true;
+#ifdef LEOEC_MEASURE
+    flipper.join();
+#endif
+    std::printf("%s: %s\n", what, g_errs.empty() ? "ok" : "FAILED");
+  };
+  phase("callers on their own devices", false);
+
+  // phase 2: spread over both devices (opt-in), then back to the default
+  {
+    int devs[2] = {0, 1};
+    if (leoec_host_spread(devs, 2) != 2) fail("leoec_host_spread({0,1}) != 2");
+    int bad = 7;
+    if (leoec_host_spread(&bad, 1) != LEOEC_E_NO_DEVICE) fail("spread to a missing device accepted");
+    phase("spread over 2 devices", true);
+    if (leoec_host_spread(nullptr, 0) != 0) fail("leoec_host_spread reset");
+  }
+
+  // phase 3: plan-cache churn: every 4-erasure pattern of vandrs(10,4,8)
+  // from 4 threads, and bitmatrix plans (cauchyrs w = 17) large enough to
+  // cross the cache's byte bound
+  {
+    Case c{LEOEC_VANDRS, 10, 4, 8, 4096};
+    prepare(&c, 7);
+    Case cb{LEOEC_CAUCHYRS, 24, 8, 20, 24 * 20 * 16 * 2};
+    prepare(&cb, 8);
+    std::vector<std::thread> th;
+    for (int t = 0; t < 4; ++t)
+      th.emplace_back([&, t] {
+        int idx = 0;
+        for (int a = 0; a < 14; ++a)
+          for (int b = a + 1; b < 14; ++b)
+            for (int d = b + 1; d < 14; ++d)
+              for (int e = d + 1; e < 14; ++e, ++idx) {
+                if (idx % 4 != t) continue;
+                std::vector<int> ids;
+                std::vector<const uint8_t*> ptrs;
+                for (int id = 0; id < 14; ++id)
+                  if (id != a && id != b && id != d && id != e) {
+                    ids.push_back(id);
+                    ptrs.push_back(block(c, id));
+                  }
+                std::vector<uint8_t> out(c.size);
+                const int rc = leoec_decode(c.coding, 10, 4, 8, ptrs.data(), ids.data(), 10, c.bs,
+                                            c.size, out.data());
+                if (rc || std::memcmp(out.data(), c.data.data(), c.size))
+                  fail("pattern decode rc " + std::to_string(rc));
+              }
+        for (int r = 0; r < 40; ++r) {
+          // distinct lost pairs of the 32-block cauchyrs code: distinct plans
+          const int x = (t * 40 + r) % 32, y = (t * 40 + r * 7 + 1) % 32;
+          if (x == y) continue;
+          std::vector<int> avail;
+          std::vector<const uint8_t*> ptrs;
+          for (int id = 0; id < 32; ++id)
+            if (id != x && id != y) {
+              avail.push_back(id);
+              ptrs.push_back(block(cb, id));
+            }
+          const int rep[2] = {x, y};
+          std::vector<uint8_t> out(2 * cb.bs);
+          const int rc = leoec_repair(cb.coding, 24, 8, 20, ptrs.data(), avail.data(),
+                                      (int)avail.size(), cb.bs, rep, 2, out.data());
+          if (rc || std::memcmp(out.data(), block(cb, x), cb.bs) ||
+              std::memcmp(out.data() + cb.bs, block(cb, y), cb.bs))
+            fail("bitmatrix repair rc " + std::to_string(rc));
+        }
+      });
+    for (auto& x : th) x.join();
+    std::printf("plan cache churn: %s\n", g_errs.empty() ? "ok" : "FAILED");
+  }
+
+  for (const auto& e : g_errs) std::fprintf(stderr, "ERROR %s\n", e.c_str());
+  std::printf("%s\n", g_errs.empty() ? "host_stress: all results bit-exact" : "host_stress: FAILED");
+  return g_errs.empty() ? 0 : 1;
+}

@@ -126,13 +126,11 @@ def main():
         for env, label in [({"LEOEC_GFBIT_LW": "1"}, "lane 4 B"),
                            ({"LEOEC_GFBIT_LW": "4"}, "lane 16 B"),
                            ({"LEOEC_BITMATRIX": "1"}, "masked bitmatrix kernel")]:
-            os.environ.update(env)
-            le._lib.measure_reload()  # knobs live in the measurement build
+            for k, v in env.items():  # knobs live in the measurement build
+                le._lib.measure_set_knob(k, v)
             stripe_case(torch, le, "cauchyrs", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], None,
                         "cfg3 variant (%s): cauchyrs(10,4,8) 1 MiB x1024" % label)
-            for k in env:
-                os.environ.pop(k)
-                le._lib.measure_reload()
+            le._lib.measure_reset_knobs()
     stripe_case(torch, le, "vandrs", 10, 4, 8, 64 * MiB, 64, R, [0, 1, 2, 3], None,
                 "cfg4: vandrs RS(10,4,8) 64 MiB x64 per GPU")
     stripe_case(torch, le, "isars", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], [0, 5, 10, 13],

@@ -57,14 +57,12 @@ def main():
     keys = {kv.split("=")[0] for v in variants for kv in v.split(",") if kv}
 
     def setenv(v):
-        for key in keys:
-            os.environ.pop(key, None)
-            le._lib.measure_reload()  # knobs live in the measurement build
+        for key in keys:  # knobs live in the measurement build (its setter)
+            le._lib.measure_set_knob(key, None)
         for kv in v.split(","):
             if kv:
                 a, b = kv.split("=")
-                os.environ[a] = b
-                le._lib.measure_reload()  # knobs live in the measurement build
+                le._lib.measure_set_knob(a, b)
 
     ops = {"encode": (lambda: le.device.encode(args.coding, p, objs, args.size, par),
                       (k + m) * bs * n)}

@@ -50,8 +50,7 @@ def main():
     cp_dst = torch.empty_like(cp_src)
     for rnd in range(args.rounds):
         for v in variants:
-            os.environ["LEOEC_GF8_VARIANT"] = str(v)
-            le._lib.measure_reload()  # knobs live in the measurement build
+            le._lib.measure_set_knob("LEOEC_GF8_VARIANT", v)  # measurement build
             evs = []
             for _ in range(args.reps):
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
@@ -76,8 +75,7 @@ def main():
             e[1].record(stream)
             torch.cuda.synchronize()
             res["d2d-copy"]["enc"].append(e[0].elapsed_time(e[1]))
-    os.environ.pop("LEOEC_GF8_VARIANT", None)
-    le._lib.measure_reload()  # knobs live in the measurement build
+    le._lib.measure_set_knob("LEOEC_GF8_VARIANT", None)
     le.device.encode("vandrs", (K, M, W), objs, size, parity)
     le.device.decode("vandrs", (K, M, W), objs, size, parity, [0, 1, 2, 3])
     torch.cuda.synchronize()

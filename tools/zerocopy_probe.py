@@ -86,14 +86,13 @@ def main():
 
     def with_env(f, env):  # measurement build: a knob set for this form only
         def g():
-            os.environ.update(env)
-            le._lib.measure_reload()
+            for k, v in env.items():
+                le._lib.measure_set_knob(k, v)
             try:
                 f()
             finally:
                 for k in env:
-                    os.environ.pop(k, None)
-                le._lib.measure_reload()
+                    le._lib.measure_set_knob(k, None)
         return g
 
     forms = [("pageable", pageable), ("dma-pinned", dma_pinned),
