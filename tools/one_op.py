@@ -21,9 +21,16 @@ def main():
     ap.add_argument("--op", choices=["encode", "decode"], default="encode")
     ap.add_argument("--erased", default="0,1,2,3")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--knobs", default="",
+                    help="K=V,K=V: measurement-build knobs (loads libleoec_measure.so)")
     args = ap.parse_args()
+    if args.knobs:  # before the package loads its library
+        os.environ["LEOEC_LIBRARY"] = "measure"
     import torch
     import leo_erasure_amd as le
+    for kv in filter(None, args.knobs.split(",")):
+        k, _, v = kv.partition("=")
+        le._lib.measure_set_knob(k, v)
     torch.cuda.set_device(0)
     assert le.gf_init() == "ok"
     p = (args.k, args.m, args.w)
