@@ -1,0 +1,58 @@
+// host_copy.hpp — the host copies that pack callers' blocks into pinned,
+// device-visible buffers (hostq.cpp batch arenas, engine.cpp zero-copy
+// staging).  Those buffers are only read by the DMA engine or by kernels
+// over PCIe, never by the CPU, so their cache lines need not be fetched or
+// kept: pack_pinned() writes them with non-temporal 32-byte stores (no
+// read-for-ownership, no cache pollution) when Knobs::hostq_ntcopy is set
+// (measurement build, A/B), plain memcpy otherwise.
+#pragma once
+
+#include <algorithm>
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+#include <immintrin.h>
+#endif
+
+#include "knobs.hpp"
+
+namespace leoec {
+
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+__attribute__((target("avx2"))) inline void stream_copy_avx2(uint8_t* d, const uint8_t* s,
+                                                             size_t n) {
+  const size_t head = std::min<size_t>((32u - ((uintptr_t)d & 31u)) & 31u, n);
+  std::memcpy(d, s, head);
+  d += head;
+  s += head;
+  n -= head;
+  size_t i = 0;
+  for (; i + 128 <= n; i += 128) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 32));
+    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 64));
+    const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 96));
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i), a);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 32), b);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 64), c);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 96), e);
+  }
+  std::memcpy(d + i, s + i, n - i);
+  _mm_sfence();  // the stores are visible before the caller publishes the fill
+}
+#endif
+
+inline void pack_pinned(void* dst, const void* src, size_t n) {
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (knobs().hostq_ntcopy && avx2 && n >= ((size_t)64 << 10)) {
+    stream_copy_avx2(static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), n);
+    return;
+  }
+#endif
+  std::memcpy(dst, src, n);
+}
+
+}  // namespace leoec

@@ -21,6 +21,7 @@
 #include <thread>
 
 #include "../../include/leoec.h"
+#include "host_copy.hpp"
 #include "knobs.hpp"
 
 namespace leoec {
@@ -507,7 +508,7 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
   q->cv_worker.notify_one();
   lk.unlock();
 
-  for (const HostSeg& g : job.in) std::memcpy(s->h_in + oi + g.off, g.src, g.n);
+  for (const HostSeg& g : job.in) pack_pinned(s->h_in + oi + g.off, g.src, g.n);
   // bytes of the region no segment covers are read by the kernels only
   // inside an aligned 16-byte chunk that also holds real bytes, and cleared
   // there (kernels_impl.hpp guarded tiles): nothing to zero

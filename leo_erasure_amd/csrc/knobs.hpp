@@ -34,6 +34,8 @@ struct Knobs {
                              //   pinned, device-mapped arenas)
   int hostq_lanes = 0;       // LEOEC_HOSTQ_LANES: dispatcher lanes (0: one per gfx950 device;
                              //   N: N lanes, lane i on device i % devices)
+  int hostq_ntcopy = 0;      // LEOEC_HOSTQ_NTCOPY=1: callers pack inputs into the pinned
+                             //   buffers with non-temporal stores (host_copy.hpp)
   // kernels.hip / kernels_impl.hpp
   int gf8_variant = 0;       // LEOEC_GF8_VARIANT: gf8_apply<10,4> variant (gf8_exp.hip)
   int gf8_tmap = 0;          // LEOEC_GF8_TMAP: gf8_apply workgroup -> tile order
