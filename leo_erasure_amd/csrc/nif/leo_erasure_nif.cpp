@@ -10,6 +10,14 @@
 // {K,M,W} arity is checked, and the NIFs run on dirty schedulers so a GPU
 // round trip never blocks a normal scheduler thread.
 //
+// load/3 (the reference has none, nif.cpp:353): the library runs a
+// host-memory call on the calling scheduler thread's current HIP device.  A
+// VM that should drive several GPUs sets LEOEC_HOST_DEVICES before starting
+// ("all", or a comma list of device ordinals): load passes the set to
+// leoec_host_spread, and calls then go to the least-loaded device of the set.
+// A malformed value fails the load; a set the runtime cannot serve (no GPU)
+// is left to the data calls, which report LEOEC_E_NO_DEVICE as usual.
+//
 // -DLEOEC_NIF_REF_ERRORS reproduces the reference's error terms exactly: its
 // coder exceptions are rethrown by value as std::exception
 // (nif.cpp:80-83,94-97,108-111), so every coder / engine failure reads
@@ -23,6 +31,7 @@
 #ifdef HAVE_ERL_NIF
 #include <erl_nif.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -211,7 +220,43 @@ ErlNifFunc nif_funcs[] = {
     {"repair", 5, nif_repair, ERL_NIF_DIRTY_JOB_IO_BOUND},
 };
 
+// LEOEC_HOST_DEVICES -> devices; false if malformed.  Unset or empty: no
+// spreading (an empty set).
+bool parse_host_devices(const char* e, std::vector<int>* devs) {
+  devs->clear();
+  if (!e || !*e) return true;
+  if (!std::strcmp(e, "all")) {
+    const int n = leoec_host_lanes(nullptr, 0);
+    if (n > 0) {
+      devs->resize((size_t)n);
+      if (leoec_host_lanes(devs->data(), n) != n) devs->clear();
+    }
+    return true;
+  }
+  for (const char* q = e; *q;) {
+    char* end = nullptr;
+    const long v = std::strtol(q, &end, 10);
+    if (end == q || v < 0 || v > 1023) return false;
+    devs->push_back((int)v);
+    q = end;
+    if (*q == ',') {
+      ++q;
+      if (!*q) return false;
+    } else if (*q) {
+      return false;
+    }
+  }
+  return true;
+}
+
+int nif_load(ErlNifEnv*, void**, ERL_NIF_TERM) {
+  std::vector<int> devs;
+  if (!parse_host_devices(std::getenv("LEOEC_HOST_DEVICES"), &devs)) return 1;
+  if (!devs.empty()) (void)leoec_host_spread(devs.data(), (int)devs.size());
+  return 0;
+}
+
 }  // namespace
 
-ERL_NIF_INIT(leo_erasure, nif_funcs, nullptr, nullptr, nullptr, nullptr)
+ERL_NIF_INIT(leo_erasure, nif_funcs, nif_load, nullptr, nullptr, nullptr)
 #endif  // HAVE_ERL_NIF

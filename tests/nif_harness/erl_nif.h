@@ -56,12 +56,18 @@ int enif_inspect_iolist_as_binary(ErlNifEnv *env, ERL_NIF_TERM t, ErlNifBinary *
 int enif_alloc_binary(size_t size, ErlNifBinary *bin);
 void enif_release_binary(ErlNifBinary *bin);
 
-/* The shim's ERL_NIF_INIT(leo_erasure, funcs, ...) exposes its table here. */
+/* The shim's ERL_NIF_INIT(leo_erasure, funcs, load, ...) exposes its table
+ * and its load callback (called as the VM would, load_info 0) here. */
 const ErlNifFunc *leoec_test_nif_table(unsigned *count);
+int leoec_test_nif_load(void);
 #define ERL_NIF_INIT(MOD, FUNCS, LOAD, RELOAD, UPGRADE, UNLOAD)                 \
   extern "C" const ErlNifFunc *leoec_test_nif_table(unsigned *count) {         \
     *count = (unsigned)(sizeof(FUNCS) / sizeof(FUNCS[0]));                     \
     return FUNCS;                                                              \
+  }                                                                            \
+  extern "C" int leoec_test_nif_load(void) {                                   \
+    int (*f)(ErlNifEnv *, void **, ERL_NIF_TERM) = LOAD;                       \
+    return f ? f(nullptr, nullptr, 0) : 0;                                     \
   }
 
 #ifdef __cplusplus

@@ -318,6 +318,7 @@ ERL_NIF_TERM h_call(const char* name, int argc, const ERL_NIF_TERM* argv, unsign
   }
   return 0;
 }
+int h_load(void) { return leoec_test_nif_load(); }
 unsigned h_nfuncs(void) {
   unsigned n = 0;
   leoec_test_nif_table(&n);

@@ -41,10 +41,12 @@ def build(outdir, defines=()):
 class Harness:
     def __init__(self, so):
         from leo_erasure_amd import _lib
+        self.path = so
         ctypes.CDLL(_lib.LIB_PATH, mode=ctypes.RTLD_GLOBAL | os.RTLD_NOLOAD)
         L = ctypes.CDLL(so)
         for name, res, args in [
             ("h_reset", None, []), ("h_live_allocs", ctypes.c_long, []),
+            ("h_load", ctypes.c_int, []),
             ("h_violations", ctypes.c_long, []),
             ("h_atom", T, [ctypes.c_char_p]), ("h_int", T, [ctypes.c_longlong]),
             ("h_bin", T, [ctypes.c_char_p, ctypes.c_size_t]),

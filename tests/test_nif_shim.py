@@ -14,6 +14,9 @@ import os
 import numpy as np
 import pytest
 
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
 from nif_harness.term import Atom, Harness, Raw, Sub, build, text  # noqa: E402
 
 ok, error = Atom("ok"), Atom("error")
@@ -324,3 +327,26 @@ def test_gpu_engine_errors_through_shim(nif, gpu, le):
     sub = Sub(r[1][0].handle, 0, 3)
     assert err(nif.call("decode", VANDRS, PARAMS, [sub] + blocks[1:10], list(range(10)),
                         len(DATA))) == le.strerror(-13)
+
+
+@pytest.mark.parametrize("spec,rc", [(None, 0), ("", 0), ("all", 0), ("0", 0), ("0,1,7", 0),
+                                     ("0,x", 1), (",", 1), ("1,", 1), ("-1", 1), ("gpu0", 1)])
+def test_load_host_devices(nif, spec, rc):
+    """The shim's load callback (the reference registers none): the
+    LEOEC_HOST_DEVICES opt-in to spreading host calls over several GPUs is
+    parsed at load; a malformed value fails the load, a well-formed one that
+    the runtime cannot serve (no GPU here) is left to the data calls.  Run in
+    a child process: the test never writes its own environment."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path[:0] = [%r, %r]\n"
+            "import leo_erasure_amd\n"
+            "from nif_harness.term import Harness\n"
+            "print(Harness(%r).L.h_load())\n") % (ROOT, HERE, nif.path)
+    env = {k: v for k, v in os.environ.items() if k != "LEOEC_HOST_DEVICES"}
+    if spec is not None:
+        env["LEOEC_HOST_DEVICES"] = spec
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         timeout=120, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert int(out.stdout.strip().splitlines()[-1]) == rc
