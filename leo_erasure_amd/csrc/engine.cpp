@@ -1023,6 +1023,7 @@ int op_decode(int coding, int k, int m, int w, const uint8_t* const* blocks, con
           std::memcpy(v.out + off, v.blocks[(*v.present)[i]], clamp_valid(v.size, off, v.bs));
       }
     }
+    bool done = false;  // copied already (before a batch that was then not used)
   } survivors{k, bs, size, blocks, &present, out};
   Staging* st = nullptr;
   uint8_t* dev = nullptr;
@@ -1044,14 +1045,23 @@ int op_decode(int coding, int k, int m, int w, const uint8_t* const* blocks, con
     for (size_t o = 0; o < want.size(); ++o)
       J.out.push_back(OutSeg{out + (uint64_t)want[o] * bs, o * bs16,
                              clamp_valid(size, (uint64_t)want[o] * bs, bs)});
-    rc = hostq_run(J, &ticket, &Survivors::copy, &survivors);
-    if (rc != kNotBatched) return rc;
+    // the surviving data blocks go into the output while the batch is on
+    // the GPU (Knobs::hostq_survivors = 1), or before the call joins the
+    // batch (0), or after its outputs are unpacked (2)
+    const int where = knobs().hostq_survivors;
+    if (where == 0) Survivors::copy(&survivors);
+    rc = hostq_run(J, &ticket, where == 1 ? &Survivors::copy : nullptr, &survivors);
+    if (rc != kNotBatched) {
+      if (rc == LEOEC_OK && where == 2) Survivors::copy(&survivors);
+      return rc;
+    }
+    if (where == 0) survivors.done = true;
     on.reset(new DeviceScope(ticket.device));
     if (!on->ok()) return LEOEC_E_HIP;
     rc = run_host_map(*plan, blocks, slot, bs, &st, &dev, &dstride);
     if (rc) return rc;
   }
-  Survivors::copy(&survivors);
+  if (!survivors.done) Survivors::copy(&survivors);
   if (!st) return LEOEC_OK;
   std::vector<D2HSeg> segs;
   for (size_t o = 0; o < want.size(); ++o) {

@@ -36,6 +36,10 @@ struct Knobs {
                              //   N: N lanes, lane i on device i % devices)
   int hostq_ntcopy = 0;      // LEOEC_HOSTQ_NTCOPY=1: callers pack inputs into the pinned
                              //   buffers with non-temporal stores (host_copy.hpp)
+  int hostq_survivors = 1;   // LEOEC_HOSTQ_SURVIVORS: where a batched decode copies its
+                             //   surviving data blocks into the output: 1 while its batch
+                             //   is on the GPU, 0 before joining the batch, 2 after its
+                             //   outputs are unpacked (the slot is freed sooner)
   // kernels.hip / kernels_impl.hpp
   int gf8_variant = 0;       // LEOEC_GF8_VARIANT: gf8_apply<10,4> variant (gf8_exp.hip)
   int gf8_tmap = 0;          // LEOEC_GF8_TMAP: gf8_apply workgroup -> tile order

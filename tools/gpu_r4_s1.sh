@@ -24,5 +24,5 @@ step r04_s1_packet_ceiling_4096 120 tools/packet_ceiling 4096 20
 step r04_s1_smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step r04_s1_pytest 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread
 step r04_s1_bench 600 python bench.py
-step r04_s1_e2e_enc_dec 600 python tools/e2e_bench.py --forms "default:;ntcopy:LEOEC_HOSTQ_NTCOPY=1;default2:" --threads 8,16,32 --no-ceiling
+step r04_s1_e2e_enc_dec 600 python tools/e2e_bench.py --forms "default:;ntcopy:LEOEC_HOSTQ_NTCOPY=1;surv0:LEOEC_HOSTQ_SURVIVORS=0;surv2:LEOEC_HOSTQ_SURVIVORS=2;default2:" --threads 8,16,32 --no-ceiling
 echo "session done"

@@ -2,7 +2,9 @@
 # Round 4, cauchyrs 16-byte swap form (gfbs_apply, LEOEC_GFBIT_FORM=4): the
 # measurement-form parity tests, an interleaved A/B against the shipped
 # 8-byte-lane kernel at 1,024 and 4,096 objects, and the vector-memory
-# instruction count of both (PMC, one pass per counter group).
+# instruction count of both (PMC, one pass per counter group); then (was
+# gpu_r4_s3.sh) configs[4]'s bench line, a 2-rank rehearsal of the N > 1
+# line, and the rocprof summaries of both bench workloads.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p $OUT
@@ -27,4 +29,13 @@ pmc cauchy_swap --coding cauchyrs --op encode --knobs LEOEC_GFBIT_FORM=4 || exit
 cd "$ROOT"
 python tools/pmc_summary.py gpurun_out/pmc_cauchy_shipped gfbit_apply > gpurun_out/pmc_cauchy_shipped.json
 python tools/pmc_summary.py gpurun_out/pmc_cauchy_swap gfbs_apply > gpurun_out/pmc_cauchy_swap.json
+cd "$ROOT"
+step r04_s3_bench64 600 python bench.py --workload 64MiB --no-cpu
+step r04_s3_bench2 600 python bench.py --gpus 2 --oversubscribe --steps 50 --warmup 10 --no-cpu
+cd /tmp && export TMPDIR=/tmp
+step r04_s3_prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/r04_prof" -o run -- python "$ROOT/bench.py" --no-cpu
+step r04_s3_prof64 600 rocprofv3 --kernel-trace --stats -d "$OUT/r04_prof64" -o run -- python "$ROOT/bench.py" --workload 64MiB --no-cpu
+cd "$ROOT"
+python tools/rocprof_summary.py "$OUT/r04_prof" > "$OUT/r04_bench_kernel_summary.txt"
+python tools/rocprof_summary.py "$OUT/r04_prof64" > "$OUT/r04_bench64_kernel_summary.txt"
 echo "session done"
