@@ -14,6 +14,8 @@ step r04_s2_swap_forms 600 python -u -m pytest tests/test_measure_forms.py -m me
 V=";LEOEC_GFBIT_FORM=4;LEOEC_GFBIT_FORM=4,LEOEC_GFBIT_PF=0;LEOEC_GFBIT_FORM=4,LEOEC_GFBIT_WG=128;LEOEC_GFBIT_FORM=4,LEOEC_GFBIT_WG=512"
 TAILN=12 step r04_s2_ab_swap_1024 600 python tools/env_ab.py --coding cauchyrs --objects 1024 --rounds 5 --variants "$V"
 TAILN=12 step r04_s2_ab_swap_4096 600 python tools/env_ab.py --coding cauchyrs --objects 4096 --rounds 3 --variants "$V"
+# host path: non-temporal packing (now shipped) against memcpy, interleaved
+TAILN=6 step r04_s2_e2e_ntcopy_ab 600 python tools/e2e_bench.py --forms "nt:;memcpy:LEOEC_HOSTQ_NTCOPY=0;nt2:;memcpy2:LEOEC_HOSTQ_NTCOPY=0" --threads 1,4,8,16,32 --no-ceiling
 unset LEOEC_LIBRARY
 cd /tmp && export TMPDIR=/tmp
 pmc() {
