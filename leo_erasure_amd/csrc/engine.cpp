@@ -873,7 +873,7 @@ int run_host_map(const Plan& plan, const uint8_t* const* blocks, const std::vect
     in[i] = Shard{base + (uint64_t)i * bs16, 0, bs};
   }
   if (zc) {
-    for (const H2DSeg& g : segs) pack_pinned(st->zh + g.dev_off, g.host, g.n);
+    for (const H2DSeg& g : segs) pack_pinned(st->zh + g.dev_off, g.host, g.n, segs.size() > 1);
   } else {
     rc = stage_h2d_segs(st, st->buf, segs);
   }
@@ -979,7 +979,7 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
   for (int j = 0; j < k; ++j)
     in[j] = Shard{base + (uint64_t)j * bs, 0, clamp_valid(size, (uint64_t)j * bs, bs)};
   for (int i = 0; i < m; ++i) par[i] = Shard{base + (uint64_t)(k + i) * bs, 0, bs};
-  if (zc) pack_pinned(st->zh, obj, size);
+  if (zc) pack_pinned(st->zh, obj, size, false);
   else rc = stage_h2d_segs(st, st->buf, {H2DSeg{obj, 0, (size_t)size}});
   if (rc == LEOEC_OK) rc = run_plan(*plan, in, par, bs, 1, st->stream);
   if (rc) {

@@ -288,152 +288,6 @@ GfbFn pick_gfba_knobs(int r) {
   return pick_gfba<64, false, 2>(r);
 }
 
-// gfbs_apply (measurement form, LEOEC_GFBIT_FORM=4; w = 8, no accumulation,
-// <= 16 inputs): the shipped 8-byte-column register layout (acc 64 VGPRs,
-// a two-block ring) fed by 16-byte memory instructions, half as many as the
-// shipped 8-byte lanes issue (profiles/r03b_v12_pmc_cauchy_alignment.json:
-// 1.95x gf8's vector-memory instructions for the same bytes).  For packet
-// pair (2p, 2p+1) lanes 0-31 of a wave load 16 B of packet 2p and lanes 32-63
-// 16 B of packet 2p+1 over the same 512-B span (raw buffer loads: chunks past
-// the block's valid length read as zeros); at consume time two
-// v_permlane32_swap_b32 per pair (dwords 0<->2 and 1<->3: lanes 32-63 of the
-// first with lanes 0-31 of the second, cdna_hip_programming.md T21) leave lane
-// l < 32 holding bytes [off, off+8) and lane l + 32 bytes [off+8, off+16) of
-// BOTH packets, the shipped layout with columns permuted over lanes.  Stores:
-// the same two swaps (an involution), then one 16-byte store per pair.  The
-// pattern (tools/packet_ceiling.hip, "swap16") checks the swaps byte for byte.
-__device__ __forceinline__ void swap_halves(uint32_t& a, uint32_t& b) {
-  const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-  a = r[0];
-  b = r[1];
-}
-
-template <int W, int R, int WG, int PF>
-__global__ void __launch_bounds__(WG) gfbs_apply(const GfbArgs<R> a) {
-  static_assert(W % 2 == 0, "packet pairs");
-  constexpr int P = W / 2;
-  const uint32_t bid = a.xmap ? xcd_obj_map(blockIdx.x, gridDim.x, a.tiles) : blockIdx.x;
-  const uint32_t obj = bid / a.tiles;
-  const uint32_t tile = bid - obj * a.tiles;
-  const uint32_t lane = threadIdx.x & 63u, half = lane >> 5;
-  const uint32_t wbase = tile * (WG * 8u) + (threadIdx.x / 64u) * 512u;
-  if (wbase >= a.ps) return;  // the whole wave is past the packet
-  // this lane's 16-byte chunk (lanes l and l + 32 share it: both live or both
-  // past ps; ps is a multiple of 16, so a live chunk lies inside its packet)
-  const uint32_t off = wbase + (lane & 31u) * 16u;
-  const uint64_t o64 = obj;
-  const int K = a.K;
-  LaneVec<2> acc[R][W];
-#pragma unroll
-  for (int i = 0; i < R; ++i)
-#pragma unroll
-    for (int x = 0; x < W; ++x) acc[i][x].v[0] = acc[i][x].v[1] = 0u;
-  auto load = [&](int j, u32x4 (&d)[P]) {
-    const DevShard s = a.in[j];
-    const auto rs = shard_rsrc(s.base, s.stride, s.valid, o64, 16u);
-#pragma unroll
-    for (int p = 0; p < P; ++p)
-      d[p] = __builtin_amdgcn_raw_buffer_load_b128(rs, (2u * p + half) * a.ps + off, 0, 2);
-  };
-  auto eat = [&](int j, u32x4 (&d)[P]) {
-    const uint32_t valid = a.in[j].valid;
-    if (valid & 15u) {  // (uniform) the chunk straddling valid: clear its tail
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        const uint32_t at = (2u * p + half) * a.ps + off;
-        if (valid < at + 16u) d[p] = keep_first(d[p], valid > at ? valid - at : 0u);
-      }
-    }
-    LaneVec<2> y[W];
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      uint32_t a0 = d[p][0], a1 = d[p][1], a2 = d[p][2], a3 = d[p][3];
-      swap_halves(a0, a2);
-      swap_halves(a1, a3);
-      y[2 * p].v[0] = a0;
-      y[2 * p].v[1] = a1;
-      y[2 * p + 1].v[0] = a2;
-      y[2 * p + 1].v[1] = a3;
-    }
-    uint32_t c[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) c[i] = a.coef[i][j];
-    gfb_accumulate<W, R, 2, false>(acc, y, c);
-  };
-  if constexpr (PF == 0) {
-    u32x4 ra[P];
-    for (int j = 0; j < K; ++j) {
-      load(j, ra);
-      eat(j, ra);
-    }
-  } else {
-    u32x4 ra[P], rb[P];
-    load(0, ra);
-    for (int j = 0;; j += 2) {
-      if (j + 1 < K) load(j + 1, rb);
-      eat(j, ra);
-      __builtin_amdgcn_sched_barrier(0);  // the next loads stay below: same registers
-      if (j + 1 >= K) break;
-      if (j + 2 < K) load(j + 2, ra);
-      eat(j + 1, rb);
-      __builtin_amdgcn_sched_barrier(0);
-      if (j + 2 >= K) break;
-    }
-  }
-  const bool live = off < a.ps;
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    uint8_t* q = const_cast<uint8_t*>(a.out[i].base) + o64 * a.out[i].stride;
-    const uint32_t ov = a.out[i].valid;
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      uint32_t a0 = acc[i][2 * p].v[0], a1 = acc[i][2 * p].v[1];
-      uint32_t a2 = acc[i][2 * p + 1].v[0], a3 = acc[i][2 * p + 1].v[1];
-      swap_halves(a0, a2);  // every lane takes part, live or not
-      swap_halves(a1, a3);
-      if (live) store_guarded(q, (2u * p + half) * a.ps + off, ov, u32x4{a0, a1, a2, a3});
-    }
-  }
-}
-
-bool gfbs_applies(int w, bool acc, int nk) { return w == 8 && !acc && nk <= kMaxK; }
-
-template <int R, int WG, int PF>
-int launch_gfbs_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
-                  hipStream_t s) {
-  GfbArgs<R> a;
-  a.K = nk;
-  a.ps = (uint32_t)(p.block_size / 8u);
-  a.tiles = packet_tiles(a.ps, WG, 8u);
-  for (int j = 0; j < kMaxK; ++j)
-    a.in[j] = j < nk ? dev_shard(p.in[j0 + j], o0) : DevShard{nullptr, 0, 0, 0};
-  for (int i = 0; i < R; ++i) {
-    a.out[i] = dev_shard(p.out[r0 + i], o0);
-    for (int j = 0; j < kMaxK; ++j)
-      a.coef[i][j] = j < nk ? p.coef[(size_t)(r0 + i) * p.K + j0 + j] : 0u;
-  }
-  a.xmap = (a.tiles <= kObjMapMaxTiles && knobs().gfbit_xmap != 0) ? 1u : 0u;
-  hipLaunchKernelGGL((gfbs_apply<8, R, WG, PF>), dim3((uint32_t)(no * a.tiles)), dim3(WG), 0, s,
-                     a);
-  return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
-}
-
-template <int WG, int PF>
-GfbFn pick_gfbs(int r) {
-  static const GfbFn tbl[kMaxR] = {&launch_gfbs_t<1, WG, PF>, &launch_gfbs_t<2, WG, PF>,
-                                   &launch_gfbs_t<3, WG, PF>, &launch_gfbs_t<4, WG, PF>};
-  return tbl[r - 1];
-}
-
-GfbFn pick_gfbs_knobs(int r) {
-  // LEOEC_GFBIT_WG = 128 | 512 (default 256); LEOEC_GFBIT_PF = 0: load, then compute
-  const Knobs& kn = knobs();
-  const bool pf0 = kn.gfbit_pf == 0;
-  if (kn.gfbit_wg == 128) return pf0 ? pick_gfbs<128, 0>(r) : pick_gfbs<128, 1>(r);
-  if (kn.gfbit_wg == 512) return pf0 ? pick_gfbs<512, 0>(r) : pick_gfbs<512, 1>(r);
-  return pf0 ? pick_gfbs<256, 0>(r) : pick_gfbs<256, 1>(r);
-}
-
 template <int W, int R, bool ACC>
 int launch_gfb_lds_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
                      hipStream_t s) {
@@ -569,8 +423,6 @@ GfbFn pick_measure(const GfBitApply& p, int w, int r, bool acc, int nk) {
   if (knobs().gfbit_form == 2 && w == 8 && r == 4 && !acc && nk <= kMaxK)
     return &launch_gfbx_8;
   if (knobs().gfbit_form == 3 && gfba_applies(p, w, acc, nk)) return pick_gfba_knobs(r);
-  // LEOEC_GFBIT_FORM=4: gfbs_apply (16-byte loads / stores, permlane32 swaps)
-  if (knobs().gfbit_form == 4 && gfbs_applies(w, acc, nk)) return pick_gfbs_knobs(r);
   if (knobs().gfbit_form == 1) {
     // LEOEC_GFBIT_WG=128: 16-byte lanes in 128-lane workgroups, next block in flight
     if (w == 8 && knobs().gfbit_wg == 128) return pick_r2<8, 4, 1, 128>(r, acc);

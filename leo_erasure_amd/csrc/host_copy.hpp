@@ -3,10 +3,14 @@
 // staging).  Those buffers are only read by the DMA engine or by kernels
 // over PCIe, never by the CPU, so their cache lines need not be fetched or
 // kept: pack_pinned() writes them with non-temporal 32-byte stores (no
-// read-for-ownership, no cache pollution).  Shipped since round 4: with 8-32
-// concurrent callers it lifts batched decode (10 survivor blocks packed per
-// call) by 6-22 % to the encode's rate (profiles/r04_s1_e2e_enc_dec.log);
-// LEOEC_HOSTQ_NTCOPY=0 (measurement build) packs with memcpy.
+// read-for-ownership, no cache pollution) when a call gathers several
+// separate host buffers (decode / repair: k survivor blocks).  Shipped since
+// round 4: in an interleaved A/B at 16 / 32 concurrent callers it lifts
+// batched decode by 12-40 % to the encode's rate (profiles/
+// r04_s2_e2e_ntcopy_ab.log, r04_s1_e2e_enc_dec.log), while an encode's one
+// contiguous 1 MiB copy read ~2 % slower with it at 32 callers, so a
+// single-segment pack keeps memcpy.  LEOEC_HOSTQ_NTCOPY=0 (measurement
+// build) packs everything with memcpy.
 #pragma once
 
 #include <algorithm>
@@ -46,13 +50,16 @@ __attribute__((target("avx2"))) inline void stream_copy_avx2(uint8_t* d, const u
 }
 #endif
 
-inline void pack_pinned(void* dst, const void* src, size_t n) {
+// gather: the copy is one of several segments of a call (see above).
+inline void pack_pinned(void* dst, const void* src, size_t n, bool gather) {
 #if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
   static const bool avx2 = __builtin_cpu_supports("avx2");
-  if (knobs().hostq_ntcopy && avx2 && n >= ((size_t)64 << 10)) {
+  if (gather && knobs().hostq_ntcopy && avx2 && n >= ((size_t)64 << 10)) {
     stream_copy_avx2(static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), n);
     return;
   }
+#else
+  (void)gather;
 #endif
   std::memcpy(dst, src, n);
 }

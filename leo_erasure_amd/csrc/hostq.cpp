@@ -508,7 +508,8 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
   q->cv_worker.notify_one();
   lk.unlock();
 
-  for (const HostSeg& g : job.in) pack_pinned(s->h_in + oi + g.off, g.src, g.n);
+  const bool gather = job.in.size() > 1;
+  for (const HostSeg& g : job.in) pack_pinned(s->h_in + oi + g.off, g.src, g.n, gather);
   // bytes of the region no segment covers are read by the kernels only
   // inside an aligned 16-byte chunk that also holds real bytes, and cleared
   // there (kernels_impl.hpp guarded tiles): nothing to zero

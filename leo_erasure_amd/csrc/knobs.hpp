@@ -34,9 +34,9 @@ struct Knobs {
                              //   pinned, device-mapped arenas)
   int hostq_lanes = 0;       // LEOEC_HOSTQ_LANES: dispatcher lanes (0: one per gfx950 device;
                              //   N: N lanes, lane i on device i % devices)
-  int hostq_ntcopy = 1;      // LEOEC_HOSTQ_NTCOPY=0: callers pack inputs into the pinned
-                             //   buffers with memcpy instead of non-temporal stores
-                             //   (host_copy.hpp; shipped since round 4)
+  int hostq_ntcopy = 1;      // LEOEC_HOSTQ_NTCOPY=0: callers pack gathered inputs (decode /
+                             //   repair) into the pinned buffers with memcpy instead of
+                             //   non-temporal stores (host_copy.hpp; shipped since round 4)
   int hostq_survivors = 1;   // LEOEC_HOSTQ_SURVIVORS: where a batched decode copies its
                              //   surviving data blocks into the output: 1 while its batch
                              //   is on the GPU, 0 before joining the batch, 2 after its

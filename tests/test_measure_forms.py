@@ -37,12 +37,7 @@ pytestmark = [pytest.mark.gpu, pytest.mark.measure_gpu]
                                  {"LEOEC_GFBIT_CBM": "1"}, {"LEOEC_GFBIT_CBM": "2"},
                                  {"LEOEC_GFBIT_CBM": "3"}, {"LEOEC_GFBIT_CBM": "4"},
                                  {"LEOEC_GFBIT_CBM": "5"},
-                                 {"LEOEC_GFBIT_FORM": "2"},  # gfbx_apply (LDS-shared, split rows)
-                                 # gfbs_apply: 16-byte loads / stores + permlane32 swaps
-                                 {"LEOEC_GFBIT_FORM": "4"},
-                                 {"LEOEC_GFBIT_FORM": "4", "LEOEC_GFBIT_PF": "0"},
-                                 {"LEOEC_GFBIT_FORM": "4", "LEOEC_GFBIT_WG": "128"},
-                                 {"LEOEC_GFBIT_FORM": "4", "LEOEC_GFBIT_WG": "512"}],
+                                 {"LEOEC_GFBIT_FORM": "2"}],  # gfbx_apply (LDS-shared, split rows)
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_cauchy_kernel_forms_agree(gpu, le, oracle, env, measure):
     """cauchyrs through the generic masked-bitmatrix kernel and through every
@@ -210,28 +205,23 @@ def test_cauchy_compiled_bitmatrix_batches(gpu, le, oracle, measure, form):
 
 @pytest.mark.parametrize("form,env", [
     ("3", {}), ("3", {"LEOEC_GFBIT_WG": "256"}), ("3", {"LEOEC_GFBIT_PF": "2"}),
-    ("3", {"LEOEC_GFBIT_PF": "3"}), ("3", {"LEOEC_GFBIT_PF": "4"}), ("3", {"LEOEC_GFBIT_PF": "5"}),
-    ("4", {}), ("4", {"LEOEC_GFBIT_PF": "0"}), ("4", {"LEOEC_GFBIT_WG": "128"}),
-    ("4", {"LEOEC_GFBIT_WG": "512"})],
+    ("3", {"LEOEC_GFBIT_PF": "3"}), ("3", {"LEOEC_GFBIT_PF": "4"}), ("3", {"LEOEC_GFBIT_PF": "5"})],
     ids=lambda e: e if isinstance(e, str) else (",".join(f"{k}={v}" for k, v in e.items()) or "default"))
 def test_cauchy_16B_forms_batches(gpu, le, oracle, measure, form, env):
-    """cauchyrs through the 16-byte-access forms: gfba_apply
+    """cauchyrs through the 16-byte-access form gfba_apply
     (LEOEC_GFBIT_FORM=3: line-aligned 16-byte copies into per-wave LDS slots,
-    read back at each packet's phase) and gfbs_apply (4: 16-byte loads and
-    stores, v_permlane32_swap half exchanges).  Object rows at every 16-byte
-    phase mod 128 (row stride = k*bs + 48), sizes whose blocks are full,
-    short (last block 103,936 of 104,960 B), one packet of 16 B, and empty
-    (size 1,040: block 9 holds nothing), and a size whose short block ends
-    mid 16-byte chunk (gfbs only: gfba needs 16-byte valid lengths); encode
-    parity equal to the shipped kernel's and to the oracle's, decode and
-    repair of erased data and parity blocks in place."""
+    read back at each packet's phase; round 4's gfbs_apply, form 4, ran here
+    too before it was removed, code at cd96abc).  Object rows at every
+    16-byte phase mod 128 (row stride = k*bs + 48), sizes whose blocks are
+    full, short (last block 103,936 of 104,960 B), one packet of 16 B, and
+    empty (size 1,040: block 9 holds nothing); encode parity equal to the
+    shipped kernel's and to the oracle's, decode and repair of erased data
+    and parity blocks in place."""
     measure.setenv("LEOEC_GFBIT_FORM", form)
     for key, v in env.items():
         measure.setenv(key, v)
     sizes = [(10, 4, 1048576), (10, 4, 1048576 - 16 * 21), (10, 4, 77776),
              (10, 4, 1040), (6, 3, 300000), (4, 2, 262144 + 4096)]
-    if form == "4":
-        sizes += [(10, 4, 1048576 - 333), (3, 2, 50001)]
     for k, m, size in sizes:
         w, n = 8, 11
         bs, _ = le.layout("cauchyrs", (k, m, w), size)
