@@ -396,11 +396,11 @@ def cpu_baseline(objs, parity, size, n_sample, target_s, ref_structure_s=None):
         pass_s = total_s / 12.0
         thr0 = _cgroup_throttled_us()
         snap0 = _cpu_snap()
-        throttled = []
+        throttled, warm = [], []
         t0 = time.perf_counter()
         rates = O.bench_rs8_pinned(K, M, host, size, ERASED, threads, cpus, pass_s, total_s,
                                    min_passes=3, parity_out=cpu_par, structure=structure,
-                                   throttled=throttled)
+                                   throttled=throttled, warm_s=total_s / 3.0, warmup=warm)
         t_all = time.perf_counter() - t0
         busy = _busy_between(snap0, _cpu_snap())
         thr1 = _cgroup_throttled_us()
@@ -408,6 +408,9 @@ def cpu_baseline(objs, parity, size, n_sample, target_s, ref_structure_s=None):
         rec.update({
             "unit": "GiB/s",
             "passes_GiBps": [round(r, 2) for r in rates],
+            # untimed: until two consecutive passes agree within 3 % (at most
+            # a third of the leg's time); a shared host ramps for seconds
+            "warmup_passes_GiBps": [round(r, 2) for r in warm],
             "throttled_s_per_pass": [None if t is None else round(t, 4) for t in throttled],
             "cgroup_throttled_s": None if thr0 is None or thr1 is None else
             round((thr1 - thr0) / 1e6, 3),
@@ -418,7 +421,8 @@ def cpu_baseline(objs, parity, size, n_sample, target_s, ref_structure_s=None):
             "sample": f"{len(rates)} passes of >= {pass_s:.2f} s over the first {n} x {size} B "
                       f"objects of rank 0's batch: vandrs RS({K},{M},8) encode + in-place "
                       f"decode of data blocks {ERASED}, {threads} threads pinned one per "
-                      f"physical core, each first-touching its own slice, {t_all:.2f} s; "
+                      f"physical core, each first-touching its own slice, after "
+                      f"{len(warm)} untimed warm-up passes; {t_all:.2f} s in all; "
                       f"value = median pass",
         })
         return rec

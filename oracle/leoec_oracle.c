@@ -13,6 +13,7 @@
 #define _GNU_SOURCE
 #include "leoec_oracle.h"
 
+#include <math.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <sched.h>
@@ -1061,7 +1062,8 @@ int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride
  * structure 0: ISA-L's one pass per object (apply_gfni / apply_avx2);
  * structure 1: Jerasure's per-(row, input) region passes (apply_regions).
  * throttled_s (nullable, max_passes): the cgroup's CFS-throttled seconds
- * during each pass, -1 where cpu.stat is unreadable. */
+ * during each pass, -1 where cpu.stat is unreadable.  warm_s > 0: untimed
+ * warm-up passes first (see below), their rates in warm_rates[0..*nwarm). */
 /* Objects are handed out from a shared counter per phase (chunks of
  * kBenchChunk), not as fixed slices: a worker whose core another tenant of
  * the host takes for a while does fewer objects instead of holding every
@@ -1168,7 +1170,8 @@ int orc_bench_rs8_pinned(int k, int m, const uint8_t *src, uint64_t src_stride, 
                          int nobj, const int *erased, int nerased, int threads, const int *cpus,
                          double pass_s, double total_s, int min_passes, double *rates,
                          int max_passes, uint8_t *parity_out, int structure,
-                         double *throttled_s) {
+                         double *throttled_s, double warm_s, double *warm_rates, int max_warm,
+                         int *nwarm) {
   if (k <= 0 || m <= 0 || k + m > 256 || threads <= 0 || threads > 256 || nerased > m ||
       nobj <= 0 || max_passes <= 0 || structure < 0 || structure > 1)
     return ORC_E_PARAMS;
@@ -1215,24 +1218,48 @@ int orc_bench_rs8_pinned(int k, int m, const uint8_t *src, uint64_t src_stride, 
   pthread_barrier_wait(&done);
   for (int t = 0; t < threads; t++) any_err |= Ws[t].err;
   double t_all = 0.0;
+  /* one pass: whole rounds until pass_s has elapsed; its GiB/s */
+#define ORC_PASS(dt_out, rate_out)                                                   \
+  do {                                                                               \
+    double t0_ = now_s(), dt_;                                                       \
+    int reps_ = 0;                                                                   \
+    do {                                                                             \
+      Q.next[0] = Q.next[1] = 0;                                                     \
+      pthread_barrier_wait(&start);                                                  \
+      pthread_barrier_wait(&done);                                                   \
+      reps_++;                                                                       \
+      dt_ = now_s() - t0_;                                                           \
+    } while (dt_ < pass_s);                                                          \
+    (dt_out) = dt_;                                                                  \
+    (rate_out) = 2.0 * (double)nobj * (double)size * reps_ / dt_ / (double)(1u << 30); \
+  } while (0)
+  /* untimed warm-up passes (the host ramps: a shared box's first passes of a
+   * run read up to 25 % low, profiles/r04_s3_bench.log): until two
+   * consecutive passes agree within 3 % or warm_s has elapsed */
+  int nw = 0;
+  for (double tw = 0.0; !any_err && warm_s > 0.0 && tw < warm_s;) {
+    double dt, r;
+    ORC_PASS(dt, r);
+    tw += dt;
+    if (warm_rates && nw < max_warm) warm_rates[nw] = r;
+    nw++;
+    if (nw >= 2 && warm_rates && nw <= max_warm &&
+        fabs(r - warm_rates[nw - 2]) <= 0.03 * warm_rates[nw - 2])
+      break;
+  }
+  if (nwarm) *nwarm = nw < max_warm ? nw : max_warm;
   while (!any_err && np < max_passes && (t_all < total_s || np < min_passes)) {
     const long long th0 = throttled_s ? cgroup_throttled_us() : -1;
-    double t0 = now_s(), dt;
-    int reps = 0;
-    do {
-      Q.next[0] = Q.next[1] = 0;
-      pthread_barrier_wait(&start);
-      pthread_barrier_wait(&done);
-      reps++;
-      dt = now_s() - t0;
-    } while (dt < pass_s);
+    double dt, r;
+    ORC_PASS(dt, r);
     t_all += dt;
     if (throttled_s) {
       const long long th1 = cgroup_throttled_us();
       throttled_s[np] = th0 < 0 || th1 < 0 ? -1.0 : (double)(th1 - th0) * 1e-6;
     }
-    rates[np++] = 2.0 * (double)nobj * (double)size * reps / dt / (double)(1u << 30);
+    rates[np++] = r;
   }
+#undef ORC_PASS
   stop = 1;
   pthread_barrier_wait(&start);
   int err = 0;

@@ -107,7 +107,8 @@ int orc_bench_rs8_pinned(int k, int m, const uint8_t *src, uint64_t src_stride, 
                          int nobj, const int *erased, int nerased, int threads, const int *cpus,
                          double pass_s, double total_s, int min_passes, double *rates,
                          int max_passes, uint8_t *parity_out, int structure,
-                         double *throttled_s);
+                         double *throttled_s, double warm_s, double *warm_rates, int max_warm,
+                         int *nwarm);
 int orc_simd_level(void);   /* 0 scalar, 2 avx2 (PSHUFB), 3 avx512bw+gfni (affine) */
 
 #ifdef __cplusplus

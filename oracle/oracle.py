@@ -63,7 +63,8 @@ def lib():
             ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_int,
             ctypes.POINTER(ctypes.c_int), ctypes.c_double, ctypes.c_double, ctypes.c_int,
             ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
-            ctypes.POINTER(ctypes.c_double)]
+            ctypes.POINTER(ctypes.c_double), ctypes.c_double, ctypes.POINTER(ctypes.c_double),
+            ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.orc_bench_rs8.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                     ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
                                     ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
@@ -216,14 +217,17 @@ def bench_rs8(op, k, m, objs, obj_stride, size, nobj, parity, erased=(), threads
 
 
 def bench_rs8_pinned(k, m, objs, size, erased, threads, cpus, pass_s, total_s, min_passes=3,
-                     max_passes=256, parity_out=None, structure=0, throttled=None):
+                     max_passes=256, parity_out=None, structure=0, throttled=None,
+                     warm_s=0.0, warmup=None):
     """bench.py's timed CPU baseline: workers pinned to `cpus`, each
     first-touching its own slice of `objs` (n x stride numpy uint8), passes of
     >= pass_s seconds of encode + in-place decode of `erased`; returns the
     per-pass GiB/s (oracle/leoec_oracle.c orc_bench_rs8_pinned).
     structure 0: ISA-L's one pass per object; 1: Jerasure's per-(row, input)
     region passes (rscoding.cpp:71 / :147).  `throttled`, a list, receives the
-    cgroup's CFS-throttled seconds per pass (None where unreadable)."""
+    cgroup's CFS-throttled seconds per pass (None where unreadable).
+    warm_s > 0: untimed warm-up passes first, until two consecutive ones agree
+    within 3 % or warm_s has elapsed; `warmup`, a list, receives their rates."""
     L = lib()
     n, stride = objs.shape[0], objs.strides[0]
     rates = (ctypes.c_double * max_passes)()
@@ -231,11 +235,15 @@ def bench_rs8_pinned(k, m, objs, size, erased, threads, cpus, pass_s, total_s, m
     er = (ctypes.c_int * max(len(erased), 1))(*erased)
     cp = (ctypes.c_int * max(len(cpus), 1))(*cpus) if cpus else None
     po = parity_out.ctypes.data if parity_out is not None else None
+    wr = (ctypes.c_double * 64)()
+    nw = ctypes.c_int(0)
     rc = L.orc_bench_rs8_pinned(k, m, objs.ctypes.data, stride, size, n, er, len(erased), threads,
                                 cp, float(pass_s), float(total_s), min_passes, rates, max_passes,
-                                po, int(structure), thr)
+                                po, int(structure), thr, float(warm_s), wr, 64, ctypes.byref(nw))
     if rc < 0:
         _chk(rc)
+    if warmup is not None:
+        warmup[:] = list(wr[:nw.value])
     if throttled is not None:
         throttled[:] = [None if t < 0 else t for t in thr[:rc]]
     return list(rates[:rc])

@@ -141,3 +141,27 @@ def test_reference_structure_parity(oracle):
     oracle.bench_rs8(0, 10, 4, objs, size, size, n, ref, threads=1)
     assert len(rates) >= 3 and len(thr) == len(rates)
     assert np.array_equal(par, ref)
+
+
+def test_warmup_passes_precede_the_timed_ones(oracle):
+    """Untimed warm-up passes (a shared host ramps for seconds): at least one
+    when warm_s > 0, at most until two agree within 3 % or warm_s elapses;
+    none when warm_s = 0; parity unaffected."""
+    n, size = 4, 100003
+    objs = np.random.default_rng(5).integers(0, 256, (n, size), dtype=np.uint8)
+    bs = oracle.block_size(10, 8, size)
+    par = np.zeros((n, 4 * bs), np.uint8)
+    ref = np.zeros_like(par)
+    warm = []
+    rates = oracle.bench_rs8_pinned(10, 4, objs, size, [0, 1, 2, 3], 2, None, 0.02, 0.06,
+                                    parity_out=par, warm_s=0.1, warmup=warm)
+    oracle.bench_rs8(0, 10, 4, objs, size, size, n, ref, threads=1)
+    assert 1 <= len(warm) <= 64 and len(rates) >= 3 and all(r > 0 for r in warm + rates)
+    # no two consecutive warm-up passes agree within 3 % before the last pair
+    for a, b in zip(warm[:-2], warm[1:-1]):
+        assert abs(b - a) > 0.03 * a
+    assert np.array_equal(par, ref)
+    warm0 = []
+    oracle.bench_rs8_pinned(10, 4, objs, size, [0, 1, 2, 3], 2, None, 0.02, 0.06,
+                            warm_s=0.0, warmup=warm0)
+    assert warm0 == []

@@ -170,6 +170,7 @@ def test_single_rank_cpu_leg_checks_parity(monkeypatch):
     # one CPU of the share left to the process's other threads
     assert cb["workers"] == cb["cores"] and cb["cores"] <= max(1, cb["share_cpus"] - 1)
     assert len(cb["throttled_s_per_pass"]) == len(cb["passes_GiBps"])
+    assert len(cb["warmup_passes_GiBps"]) >= 1
     # the reference's own CPU structure, same sample, same parity check
     rs = cb["reference_structure"]
     assert rs["parity_vs_gpu"] == {"objects": 3, "equal": True}
