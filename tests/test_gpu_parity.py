@@ -511,3 +511,27 @@ def test_measurement_forms_in_own_process(gpu):
     summary = tail.strip().splitlines()[-1]
     assert "passed" in summary and "skipped" not in summary, summary
 
+
+
+def test_host_spread_opt_in(gpu, le, oracle):
+    """leoec_host_spread: host-memory calls run on the caller's current device
+    by default; spreading over an explicit device set is opt-in, a device the
+    process cannot use is refused (the setting unchanged), and the empty set
+    restores the default.  Every call in every mode is bit-exact."""
+    devs = le._lib.host_lanes()
+    assert devs and len(devs) == gpu.cuda.device_count()
+    data = rand_bytes(1048576 + 77, 4321)
+    ref = oracle.encode("vandrs", 10, 4, 8, data)
+    try:
+        assert le._lib.host_spread(devs) == len(devs)
+        st, blocks = le.nif_encode("vandrs", (10, 4, 8), data, len(data))
+        assert st == "ok" and blocks == ref
+        with pytest.raises(le.LeoecError):
+            le._lib.host_spread([len(devs) + 7])
+        st, blocks = le.nif_encode("vandrs", (10, 4, 8), data, len(data))
+        assert st == "ok" and blocks == ref
+    finally:
+        assert le._lib.host_spread([]) == 0
+    ids = list(range(4, 14))
+    st, out = le.nif_decode("vandrs", (10, 4, 8), [ref[i] for i in ids], ids, len(data))
+    assert st == "ok" and out == data
