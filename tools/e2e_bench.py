@@ -15,7 +15,10 @@ recorded in DESIGN.md (never as the bench value):
   the pinned, batched device-API path (H2D -> leoec_encode_dev -> D2H on two
   streams) as the link ceiling.
 
-    python tools/e2e_bench.py [--quick]
+    python tools/e2e_bench.py [--quick] [--spread]
+
+--spread: host calls spread over every gfx950 device of the node
+(leoec_host_spread), for the node-level host rate.
 """
 import json
 import os
@@ -197,6 +200,9 @@ def main():
     assert le.gf_init() == "ok"
     bs, filled = le.layout("vandrs", (K, M, W), SIZE)
     quick = "--quick" in sys.argv
+    if "--spread" in sys.argv:  # every gfx950 device of the node (leoec_host_spread)
+        print(json.dumps({"spread_over_devices": le._lib.host_lanes(),
+                          "lanes": le._lib.host_spread(le._lib.host_lanes())}), flush=True)
     if "--libs" in sys.argv:  # --libs "tag:path;tag2:path2" [--threads ..] [--rounds R]
         # libraries A/B in one process, interleaved rounds (no knobs)
         libs = [e.partition(":")[::2] for e in sys.argv[sys.argv.index("--libs") + 1].split(";")]
