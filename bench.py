@@ -219,7 +219,7 @@ def cpu_share():
     except (OSError, ValueError):
         quota = None
     if quota:
-        share, basis = min(aff, int(math.floor(quota))), "cgroup cpu.max quota"
+        share, basis = max(1, min(aff, int(math.floor(quota)))), "cgroup cpu.max quota"
     else:
         share, basis = min(aff, BOX_CPU_SHARE), (
             f"affinity, capped at {BOX_CPU_SHARE} = the GPU box's CPU share per GPU")

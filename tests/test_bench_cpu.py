@@ -99,21 +99,26 @@ def test_headroom_rule(share, workers):
     assert bench.headroom_workers(share) == workers
 
 
-def test_cpu_share_leaves_one_cpu(tmp_path, monkeypatch):
+@pytest.mark.parametrize("quota,threads,share_cpus", [("1600000 100000", 15, 16),
+                                                     ("50000 100000", 1, 1),
+                                                     ("max 100000", 15, 16)])
+def test_cpu_share_leaves_one_cpu(tmp_path, monkeypatch, quota, threads, share_cpus):
+    """16-CPU quota: 15 workers; a quota under one CPU still runs one worker
+    (no negative reservation); no quota: the box's per-GPU share of 16."""
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(64)))
     real_open = open
 
     def fake_open(path, *a, **k):
         if path == "/sys/fs/cgroup/cpu.max":
             f = tmp_path / "cpu.max"
-            f.write_text("1600000 100000\n")
+            f.write_text(quota + "\n")
             return real_open(f, *a, **k)
         return real_open(path, *a, **k)
 
     monkeypatch.setattr("builtins.open", fake_open)
-    threads, share = bench.cpu_share()
-    assert share["cgroup_cpus"] == 16.0 and share["share_cpus"] == 16
-    assert threads == 15 and share["reserved_cpus"] == 1
+    t, share = bench.cpu_share()
+    assert t == threads and share["share_cpus"] == share_cpus
+    assert share["reserved_cpus"] == share_cpus - threads >= 0
 
 
 def test_throttled_passes_are_excluded():
