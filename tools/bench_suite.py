@@ -131,6 +131,8 @@ def main():
             stripe_case(torch, le, "cauchyrs", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], None,
                         "cfg3 variant (%s): cauchyrs(10,4,8) 1 MiB x1024" % label)
             le._lib.measure_reset_knobs()
+    stripe_case(torch, le, "cauchyrs", 4, 2, 3, MiB, 1024, R, [0, 1], [0, 5],
+                "cauchyrs(4,2,3) 1 MiB x1024 (the reference's default cauchyrs parameters)")
     stripe_case(torch, le, "vandrs", 10, 4, 8, 64 * MiB, 64, R, [0, 1, 2, 3], None,
                 "cfg4: vandrs RS(10,4,8) 64 MiB x64 per GPU")
     stripe_case(torch, le, "isars", 10, 4, 8, MiB, 1024, R, [0, 1, 2, 3], [0, 5, 10, 13],
