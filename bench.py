@@ -374,7 +374,8 @@ def cpu_baseline(objs, parity, size, n_sample, target_s, ref_structure_s=None):
     own CPU structure (Jerasure's per-(row, input) region passes with
     destination read-modify-write, rscoding.cpp:71 / :147; structure 1) on
     the same sample, workers and parity check, for `ref_structure_s`
-    seconds (default target_s / 2)."""
+    seconds (default target_s / 2); and a short scalar leg (the same one
+    pass with scalar table lookups, SURVEY §8(d)'s scalar reference)."""
     import numpy as np
 
     from oracle import oracle as O
@@ -448,6 +449,12 @@ def cpu_baseline(objs, parity, size, n_sample, target_s, ref_structure_s=None):
                       "(rscoding.cpp:71, :147)"),
     })
     rec["reference_structure"] = rs
+    # SURVEY §8(d)'s scalar reference: the one pass with scalar split-table
+    # lookups (no SIMD), a short leg for scale
+    sc = leg(2, target_s / 6.0 if ref_structure_s is None else ref_structure_s / 3.0)
+    sc.update({"cores": threads, "kind": "port", "simd": "scalar",
+               "structure": "one pass per object, scalar 4-bit split-table lookups"})
+    rec["scalar"] = sc
     return rec
 
 
@@ -662,7 +669,8 @@ def run_rank(args, be, rank, world, dist=None):
         except Exception as e:  # a host problem must not discard the GPU measurement
             cb = {"value": None, "error": f"{type(e).__name__}: {e}"}
         rec["cpu_baseline"] = cb
-        checked = [c for c in (cb, cb.get("reference_structure") or {}) if "parity_vs_gpu" in c]
+        checked = [c for c in (cb, cb.get("reference_structure") or {}, cb.get("scalar") or {})
+                   if "parity_vs_gpu" in c]
         rec["cpu_parity_checked"] = bool(checked)
         verified = verified and all(c["parity_vs_gpu"]["equal"] for c in checked)
     else:

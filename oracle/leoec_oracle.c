@@ -821,7 +821,8 @@ typedef struct {
   const int *surv;      /* decode: survivor ids */
   const uint32_t *coef; /* nout x k coefficients (structure 1: ones are copies / xors) */
   int structure;        /* 0: one pass over all rows (ISA-L ec_encode_data);
-                           1: Jerasure's per-(row, input) region passes */
+                           1: Jerasure's per-(row, input) region passes;
+                           2: the one pass with scalar table lookups */
 } bench_job;
 
 /* Jerasure's structure (jerasure_matrix_encode -> jerasure_matrix_dotprod per
@@ -926,6 +927,7 @@ static void bench_object_at(const bench_job *J, const uint8_t *obj, uint8_t *par
       for (int i = 0; i < J->nout; i++) out[i] = (uint8_t *)blk[J->want[i]];
     }
     if (J->structure == 1) apply_regions(nin, J->nout, J->coef, J->tbl, J->simd, in, out, bs);
+    else if (J->structure == 2) apply_scalar(nin, J->nout, J->tbl, in, out, bs);
     else
 #if defined(__x86_64__)
     if (J->simd >= 3) apply_gfni(nin, J->nout, J->mats, J->tbl, in, out, bs);
@@ -1060,6 +1062,7 @@ int orc_bench_rs8(int op, int k, int m, const uint8_t *objs, uint64_t obj_stride
  * of passes (<= max_passes) or a negative ORC_E_*.  parity_out (nobj x m x
  * bs) receives the workers' encode of the sample, for the parity check.
  * structure 0: ISA-L's one pass per object (apply_gfni / apply_avx2);
+ * structure 2: the same pass with scalar split-table lookups (apply_scalar);
  * structure 1: Jerasure's per-(row, input) region passes (apply_regions).
  * throttled_s (nullable, max_passes): the cgroup's CFS-throttled seconds
  * during each pass, -1 where cpu.stat is unreadable.  warm_s > 0: untimed
@@ -1173,7 +1176,7 @@ int orc_bench_rs8_pinned(int k, int m, const uint8_t *src, uint64_t src_stride, 
                          double *throttled_s, double warm_s, double *warm_rates, int max_warm,
                          int *nwarm) {
   if (k <= 0 || m <= 0 || k + m > 256 || threads <= 0 || threads > 256 || nerased > m ||
-      nobj <= 0 || max_passes <= 0 || structure < 0 || structure > 1)
+      nobj <= 0 || max_passes <= 0 || structure < 0 || structure > 2)
     return ORC_E_PARAMS;
   uint64_t bs = orc_block_size(k, 8, size);
   bench_plan PE, PD;

@@ -224,7 +224,8 @@ def bench_rs8_pinned(k, m, objs, size, erased, threads, cpus, pass_s, total_s, m
     >= pass_s seconds of encode + in-place decode of `erased`; returns the
     per-pass GiB/s (oracle/leoec_oracle.c orc_bench_rs8_pinned).
     structure 0: ISA-L's one pass per object; 1: Jerasure's per-(row, input)
-    region passes (rscoding.cpp:71 / :147).  `throttled`, a list, receives the
+    region passes (rscoding.cpp:71 / :147); 2: the one pass with scalar
+    table lookups (SURVEY §8(d)'s scalar reference).  `throttled`, a list, receives the
     cgroup's CFS-throttled seconds per pass (None where unreadable).
     warm_s > 0: untimed warm-up passes first, until two consecutive ones agree
     within 3 % or warm_s has elapsed; `warmup`, a list, receives their rates."""

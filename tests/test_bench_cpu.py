@@ -132,9 +132,10 @@ def test_throttled_passes_are_excluded():
     assert s["passes_used"].startswith("all") and s["value"] == 90.0
 
 
-def test_reference_structure_parity(oracle):
-    """The Jerasure-structure leg (per-(row, input) region passes) writes the
-    same parity as the one-pass leg and the oracle."""
+@pytest.mark.parametrize("structure", [1, 2])
+def test_reference_structure_parity(oracle, structure):
+    """The Jerasure-structure leg (per-(row, input) region passes, 1) and the
+    scalar leg (2) write the same parity as the one-pass leg and the oracle."""
     n, size = 6, 200003
     objs = np.random.default_rng(3).integers(0, 256, (n, size), dtype=np.uint8)
     bs = oracle.block_size(10, 8, size)
@@ -142,7 +143,7 @@ def test_reference_structure_parity(oracle):
     ref = np.zeros_like(par)
     thr = []
     rates = oracle.bench_rs8_pinned(10, 4, objs, size, [0, 1, 2, 3], 2, None, 0.02, 0.06,
-                                    parity_out=par, structure=1, throttled=thr)
+                                    parity_out=par, structure=structure, throttled=thr)
     oracle.bench_rs8(0, 10, 4, objs, size, size, n, ref, threads=1)
     assert len(rates) >= 3 and len(thr) == len(rates)
     assert np.array_equal(par, ref)

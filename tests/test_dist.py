@@ -175,6 +175,8 @@ def test_single_rank_cpu_leg_checks_parity(monkeypatch):
     rs = cb["reference_structure"]
     assert rs["parity_vs_gpu"] == {"objects": 3, "equal": True}
     assert rs["value"] > 0 and "Jerasure" in rs["structure"] and rs["cores"] == cb["cores"]
+    sc = cb["scalar"]
+    assert sc["parity_vs_gpu"] == {"objects": 3, "equal": True} and sc["simd"] == "scalar"
     assert rec["cpu_parity_checked"] is True
 
 
