@@ -54,7 +54,10 @@ def host_path(le, np, reps, tag):
     for cls, params in CLASSES:
         k, m, w = params
         bs, filled = le.layout(cls, params, SIZE)
-        src = np.zeros(SIZE, dtype=np.uint8)
+        # the eunit test's <<0:ChunkSizeBits>> is a fresh, zero-written binary:
+        # written here too (np.zeros would leave the pages untouched, and the
+        # first copy would pay their faults)
+        src = np.full(SIZE, 0, dtype=np.uint8)
         out = np.full((k + m - filled) * bs, 0xA5, dtype=np.uint8)
         cold = host_call(le, cls, params, src, out)
         assert not out.any(), f"{cls}: non-zero output for an all-zero object"
@@ -129,10 +132,44 @@ def copies(le, torch, reps):
                               "ms": round(t * 1e3, 2), "GBps": round(n / t / 1e9, 2)}), flush=True)
 
 
+def registered(torch, np, reps):
+    """hipHostRegister of a pageable 100 MiB buffer in place (what a large
+    call could do instead of bounce-buffer copies): the register and
+    unregister costs, and the H2D rate from the registered pages."""
+    rt = torch.cuda.cudart()
+    h = np.zeros(SIZE, dtype=np.uint8)
+    d = torch.empty(SIZE, dtype=torch.uint8, device="cuda")
+    reg, unreg, h2d = [], [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        rc = rt.cudaHostRegister(h.ctypes.data, SIZE, 0)
+        t1 = time.perf_counter()
+        code = int(getattr(rc, "value", rc))
+        if code != 0:
+            print(json.dumps({"bench": "hipHostRegister", "error": code}), flush=True)
+            return
+        ht = torch.from_numpy(h)
+        d.copy_(ht, non_blocking=True)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        rt.cudaHostUnregister(h.ctypes.data)
+        t3 = time.perf_counter()
+        reg.append(t1 - t0)
+        h2d.append(t2 - t1)
+        unreg.append(t3 - t2)
+    print(json.dumps({"bench": "hipHostRegister of a pageable 100 MiB buffer",
+                      "register_ms": round(statistics.median(reg) * 1e3, 2),
+                      "h2d_ms": round(statistics.median(h2d) * 1e3, 2),
+                      "h2d_GBps": round(SIZE / statistics.median(h2d) / 1e9, 2),
+                      "unregister_ms": round(statistics.median(unreg) * 1e3, 2)}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--forms", action="store_true")
+    ap.add_argument("--cold-only", action="store_true",
+                    help="gf_init and the first / warm calls only (a short target for a trace)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -140,10 +177,17 @@ def main():
         os.environ.setdefault("LEOEC_LIBRARY", "measure")
     import leo_erasure_amd as le
     torch.cuda.set_device(0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     assert le.gf_init() == "ok"
+    print(json.dumps({"bench": "gf_init", "ms": round((time.perf_counter() - t0) * 1e3, 2)}),
+          flush=True)
     host_path(le, np, args.reps, "default")
+    if args.cold_only:
+        return
     device_path(le, torch, args.reps)
     copies(le, torch, args.reps)
+    registered(torch, np, args.reps)
     if args.forms:
         for tag, env in (("pinned ring 4 MiB", {"LEOEC_HOST_STAGING": "pinned",
                                                 "LEOEC_STAGE_CHUNK_KIB": "4096"}),
