@@ -70,7 +70,10 @@ const char *leoec_strerror(int status);
 /* ---- the NIF surface ---------------------------------------------------- */
 
 /* gf_init/0 (c_src/leo_erasure_nif.cpp:122-128): build the GF(2^8/16/32)
- * host tables and open the HIP device.  Idempotent; other calls do it lazily. */
+ * host tables, open the HIP device and warm the caller's current device once
+ * (its hardware queues, the runtime's pageable-copy staging, every kernel
+ * code object: ~0.1-0.2 s) so the first encode of the VM is not charged for
+ * them.  Idempotent; other calls open the device lazily (without the warm-up). */
 int leoec_gf_init(void);
 
 /* Coder::checkParams of the class (rscoding.cpp:29-34, cauchycoding.cpp:30-35,

@@ -52,10 +52,15 @@ const char* leoec_strerror(int status) {
   }
 }
 
+// gf_init/0 (nif.cpp:122-128): the field tables, then the device runtime
+// warmed on the caller's current device (engine.cpp warm_device), so the
+// VM's first encode does not pay the runtime's lazy set-up.
 int leoec_gf_init(void) {
   return guarded([] {
     for (int w : {8, 16, 32}) (void)leoec::field(w);
-    return leoec::device_init();
+    const int rc = leoec::device_init();
+    if (rc == LEOEC_OK) (void)leoec::warm_device();
+    return rc;
   });
 }
 

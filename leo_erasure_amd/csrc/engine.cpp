@@ -487,6 +487,8 @@ struct Staging {
   uint8_t* zd = nullptr;    //   the same memory's device address
   size_t zcap = 0;
   bool zc = false;          // this call's device pointers are in [zd, zd + zcap)
+  std::vector<uintptr_t> pins;  // registrations this call uses (pin_acquire), released
+                                // once its copies are done (pins_release)
 
   Staging() = default;
   Staging(const Staging&) = delete;
@@ -655,14 +657,109 @@ bool ring_ready(Staging* st) {
   return true;
 }
 
-// Host -> device, ordered on st->stream; returns once `src` may be reused.
-int stage_h2d(Staging* st, uint8_t* dev, const uint8_t* src, size_t n) {
-  if (n == 0) return LEOEC_OK;
-  if (!ring_ready(st)) {
-    if (hipMemcpyAsync(dev, src, n, hipMemcpyHostToDevice, st->stream) != hipSuccess)
-      return LEOEC_E_HIP;
+// Caller memory pinned in place for the copies of one large call
+// (Knobs::host_pin).  Pages are pinned with hipHostRegister in page-aligned,
+// non-overlapping registrations with a user count: a call pins the gaps of
+// its range that no registration covers yet and joins the ones that do
+// (decode survivors are often sub-binaries of one parent binary, sharing
+// pages at their edges; concurrent calls on one binary share its
+// registrations), and a registration is released when its last user's
+// copies are done.  Copies are cut at registration edges, so each lies in
+// one registration.  A range the runtime refuses to pin (the host
+// application registered it itself) is copied as pageable memory, which the
+// runtime stages through its own buffers.
+struct PinnedRange {
+  uintptr_t hi;
+  int users;
+};
+std::mutex g_pin_mu;
+std::map<uintptr_t, PinnedRange> g_pins;  // lo -> range
+constexpr uintptr_t kPage = 4096;
+constexpr size_t kPinMin = (size_t)1 << 20;
+
+// Pins [p, p + n); on success appends the registration edges inside the
+// range to `cuts` (ascending) and the registrations used to st->pins.
+bool pin_acquire(Staging* st, const void* p, size_t n, std::vector<uintptr_t>* cuts) {
+  const uintptr_t lo = (uintptr_t)p & ~(kPage - 1);
+  const uintptr_t hi = ((uintptr_t)p + n + kPage - 1) & ~(kPage - 1);
+  std::lock_guard<std::mutex> l(g_pin_mu);
+  std::vector<std::pair<uintptr_t, uintptr_t>> gaps;
+  std::vector<uintptr_t> joined;
+  auto it = g_pins.upper_bound(lo);
+  if (it != g_pins.begin() && std::prev(it)->second.hi > lo) --it;
+  uintptr_t cur = lo;
+  for (; it != g_pins.end() && it->first < hi; ++it) {
+    if (it->first > cur) gaps.emplace_back(cur, it->first);
+    joined.push_back(it->first);
+    cur = std::max(cur, it->second.hi);
+  }
+  if (cur < hi) gaps.emplace_back(cur, hi);
+  for (size_t g = 0; g < gaps.size(); ++g) {
+    if (hipHostRegister(reinterpret_cast<void*>(gaps[g].first), gaps[g].second - gaps[g].first,
+                        hipHostRegisterPortable) != hipSuccess) {
+      (void)hipGetLastError();
+      for (size_t u = 0; u < g; ++u) (void)hipHostUnregister(reinterpret_cast<void*>(gaps[u].first));
+      return false;
+    }
+  }
+  for (const auto& g : gaps) {
+    g_pins[g.first] = PinnedRange{g.second, 1};
+    st->pins.push_back(g.first);
+  }
+  for (uintptr_t j : joined) {
+    ++g_pins[j].users;
+    st->pins.push_back(j);
+  }
+  for (auto r = g_pins.upper_bound((uintptr_t)p); r != g_pins.end() && r->first < (uintptr_t)p + n;
+       ++r)
+    cuts->push_back(r->first);
+  return true;
+}
+
+// After the call's copies have completed (its stream synchronised).
+void pins_release(Staging* st) {
+  if (st->pins.empty()) return;
+  std::lock_guard<std::mutex> l(g_pin_mu);
+  for (uintptr_t lo : st->pins) {
+    auto it = g_pins.find(lo);
+    if (it != g_pins.end() && --it->second.users == 0) {
+      (void)hipHostUnregister(reinterpret_cast<void*>(lo));
+      g_pins.erase(it);
+    }
+  }
+  st->pins.clear();
+}
+
+// One host <-> device copy of a large segment on st->stream: from pinned
+// caller memory in pieces of at most Knobs::host_pin_kib (0: no bound), cut
+// at registration edges; else one pageable copy.
+int copy_large(Staging* st, void* dst, const void* src, size_t n, hipMemcpyKind kind) {
+  const bool h2d = kind == hipMemcpyHostToDevice;
+  const uint8_t* host = static_cast<const uint8_t*>(h2d ? src : dst);
+  std::vector<uintptr_t> cuts;
+  if (knobs().host_pin && n >= kPinMin && pin_acquire(st, host, n, &cuts)) {
+    const size_t piece = knobs().host_pin_kib > 0 ? (size_t)knobs().host_pin_kib << 10 : n;
+    cuts.push_back((uintptr_t)host + n);
+    size_t off = 0;
+    for (uintptr_t edge : cuts) {
+      const size_t stop = (size_t)(edge - (uintptr_t)host);
+      for (; off < stop; off += std::min(piece, stop - off)) {
+        const size_t len = std::min(piece, stop - off);
+        if (hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, static_cast<const uint8_t*>(src) + off,
+                           len, kind, st->stream) != hipSuccess)
+          return LEOEC_E_HIP;
+      }
+    }
     return LEOEC_OK;
   }
+  return hip_ok(hipMemcpyAsync(dst, src, n, kind, st->stream));
+}
+
+// Host -> device, ordered on st->stream; returns once `src` may be reused
+// (a pinned source: once the stream is synchronised, before pins_release).
+int stage_h2d(Staging* st, uint8_t* dev, const uint8_t* src, size_t n) {
+  if (n == 0) return LEOEC_OK;
+  if (!ring_ready(st)) return copy_large(st, dev, src, n, hipMemcpyHostToDevice);
   for (size_t off = 0; off < n; off += st->chunk) {
     const size_t len = std::min(st->chunk, n - off);
     const int s = st->next;
@@ -705,7 +802,7 @@ struct D2HSeg {
 
 // Device -> host of every segment after the work already on st->stream, then
 // wait for the stream: on return every byte is in host memory.
-int stage_d2h_sync(Staging* st, const std::vector<D2HSeg>& segs) {
+int stage_d2h_sync_impl(Staging* st, const std::vector<D2HSeg>& segs) {
   if (st->zc) {  // outputs are in the mapped buffer: wait, then host copies
     st->zc = false;
     if (hipStreamSynchronize(st->stream) != hipSuccess) return LEOEC_E_HIP;
@@ -729,11 +826,12 @@ int stage_d2h_sync(Staging* st, const std::vector<D2HSeg>& segs) {
     }
   }
   if (!ring_ready(st)) {
+    int rc = LEOEC_OK;
     for (const D2HSeg& g : segs)
-      if (g.n && hipMemcpyAsync(g.host, g.dev, g.n, hipMemcpyDeviceToHost, st->stream) !=
-                     hipSuccess)
-        return LEOEC_E_HIP;
-    return hip_ok(hipStreamSynchronize(st->stream));
+      if (g.n && (rc = copy_large(st, g.host, g.dev, g.n, hipMemcpyDeviceToHost))) break;
+    const int sync = hip_ok(hipStreamSynchronize(st->stream));
+    pins_release(st);
+    return rc ? rc : sync;
   }
   struct Piece {
     uint8_t* host;
@@ -773,6 +871,18 @@ int stage_d2h_sync(Staging* st, const std::vector<D2HSeg>& segs) {
     }
   }
   return hip_ok(hipStreamSynchronize(st->stream));
+}
+
+// ... and the caller memory the call pinned is released once nothing of the
+// call is in flight (every path above ends in a synchronised stream but an
+// early error return).
+int stage_d2h_sync(Staging* st, const std::vector<D2HSeg>& segs) {
+  const int rc = stage_d2h_sync_impl(st, segs);
+  if (!st->pins.empty()) {
+    (void)hipStreamSynchronize(st->stream);
+    pins_release(st);
+  }
+  return rc;
 }
 
 // This thread's staging on its current device (stream only: the buffers
@@ -884,6 +994,7 @@ int run_host_map(const Plan& plan, const uint8_t* const* blocks, const std::vect
     // copies already queued may still read this thread's pinned buffer:
     // drain them before the next call reuses it
     (void)hipStreamSynchronize(st->stream);
+    pins_release(st);
     st->zc = false;
     return rc;
   }
@@ -984,6 +1095,7 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
   if (rc == LEOEC_OK) rc = run_plan(*plan, in, par, bs, 1, st->stream);
   if (rc) {
     (void)hipStreamSynchronize(st->stream);  // queued copies may still read the caller's object
+    pins_release(st);
     st->zc = false;
     return rc;
   }
@@ -1216,6 +1328,52 @@ int op_repair_dev(int coding, int k, int m, int w, const uint8_t* const* blocks,
   for (int i = 0; i < k; ++i) in[i] = Shard{blocks[surv[i]], block_stride, bs};
   for (int r = 0; r < nrep; ++r) o[r] = Shard{out[r], out_stride, bs};
   return apply(*c, surv.data(), in, want.data(), o, bs, nobj, s);
+}
+
+// ---------------------------------------------------------------------------
+// Runtime warm-up, once per device, from gf_init (the NIF's once-per-VM
+// initialisation, c_src/leo_erasure_nif.cpp:122-128).  The first call of a
+// fresh process otherwise pays the runtime's own lazy set-up inside the
+// caller's timing (profiles/r04_s7_cold_trace: the reference's 100 MiB encode
+// benchmark, 151 ms for a 2.7 ms call): the process's first stream creates
+// the device's hardware queues (92 ms), the first pageable copy sets up the
+// runtime's staging (8 ms), and each kernel code object loads at its first
+// launch (1-2 ms each).  Here, on the caller's current device: this thread's
+// staging stream, one small pageable copy each way, and one small launch
+// into every kernel code object of the library (gf8 for K = 1..16, the
+// packet-bitsliced kernel for w = 2..16, liberation / bitmatrix, w = 16/32)
+// on a scratch buffer.  Best effort: a failure here is not an error (each
+// call reports its own).
+int warm_device() {
+  if (device_init() != LEOEC_OK) return LEOEC_OK;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return LEOEC_OK;
+  static std::once_flag once[kMaxDevices];
+  std::call_once(once[dev], [] {
+    Staging* st;
+    if (get_staging(&st)) return;
+    constexpr size_t kScratch = 256u << 10, kPar = 128u << 10;
+    uint8_t* d = nullptr;
+    if (hipMalloc(&d, kScratch) != hipSuccess) return;
+    std::vector<uint8_t> h(kScratch, 0);
+    if (hipMemcpyAsync(d, h.data(), kScratch, hipMemcpyHostToDevice, st->stream) == hipSuccess) {
+      struct Warm {
+        int coding, k, m, w;
+      };
+      std::vector<Warm> codes;
+      for (int K = 1; K <= 16; ++K) codes.push_back({LEOEC_VANDRS, K, 1, 8});
+      for (int w = 2; w <= 16; ++w) codes.push_back({LEOEC_CAUCHYRS, 2, 1, w});
+      codes.push_back({LEOEC_LIBERATION, 2, 2, 3});
+      codes.push_back({LEOEC_VANDRS, 2, 1, 16});
+      codes.push_back({LEOEC_VANDRS, 2, 1, 32});
+      for (const Warm& c : codes)
+        (void)op_encode_dev(c.coding, c.k, c.m, c.w, d, kPar, 1024, 1, d + kPar, kPar, st->stream);
+      (void)hipMemcpyAsync(h.data(), d + kPar, 4096, hipMemcpyDeviceToHost, st->stream);
+    }
+    (void)hipStreamSynchronize(st->stream);
+    (void)hipFree(d);
+  });
+  return LEOEC_OK;
 }
 
 }  // namespace leoec

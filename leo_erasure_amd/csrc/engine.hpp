@@ -102,4 +102,9 @@ int op_repair_dev(int coding, int k, int m, int w, const uint8_t* const* blocks,
                   uint64_t block_stride, uint64_t bs, uint64_t nobj, const int* rep, int nrep,
                   uint8_t* const* out, uint64_t out_stride, hipStream_t s);
 
+// gf_init's runtime warm-up on the caller's current device (once per
+// device; best effort, always LEOEC_OK): hardware queues, the pageable-copy
+// staging, every kernel code object.
+int warm_device();
+
 }  // namespace leoec

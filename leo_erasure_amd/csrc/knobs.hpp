@@ -17,6 +17,11 @@ struct Knobs {
   int host_staging = 0;      // LEOEC_HOST_STAGING: 0 auto, 1 pageable, 2 gather, 3 pinned ring,
                              //   4 zero-copy (kernels on pinned, device-mapped host memory)
   int stage_chunk_kib = 256; // LEOEC_STAGE_CHUNK_KIB: pinned-ring chunk
+  int host_pin = 0;          // LEOEC_HOST_PIN=1: a per-thread copy of >= 1 MiB from / to the
+                             //   caller's memory pins that memory in place (hipHostRegister,
+                             //   refcounted) and copies it in pieces of LEOEC_HOST_PIN_KIB
+                             //   (0: one copy per segment) instead of a pageable copy
+  int host_pin_kib = 0;
   int host_batch = 1;        // LEOEC_HOST_BATCH=0: host calls take the per-thread path only
   int batch_window_us = 0;   // LEOEC_BATCH_WINDOW_US: hold an idle-GPU batch open this long
   int hostq_depth = 3;       // LEOEC_HOSTQ_DEPTH: batches on the GPU at once

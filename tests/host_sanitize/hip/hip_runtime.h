@@ -26,6 +26,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -41,6 +42,8 @@ typedef enum hipError_t {
   hipErrorOutOfMemory = 2,
   hipErrorInvalidDevice = 101,
   hipErrorNotReady = 600,
+  hipErrorHostMemoryAlreadyRegistered = 712,
+  hipErrorHostMemoryNotRegistered = 713,
 } hipError_t;
 
 typedef enum hipMemcpyKind {
@@ -56,6 +59,8 @@ typedef enum hipMemcpyKind {
 #define hipEventDisableTiming 0x2
 #define hipHostMallocDefault 0x0
 #define hipHostMallocMapped 0x2
+#define hipHostRegisterDefault 0x0
+#define hipHostRegisterPortable 0x1
 
 struct hipDeviceProp_t {
   char name[256];
@@ -142,14 +147,27 @@ inline Stream* null_stream() {
 
 struct Pinned {
   std::mutex mu;
-  std::map<uintptr_t, size_t> blocks;  // base -> bytes
+  std::map<uintptr_t, size_t> blocks;  // base -> bytes (hipHostMalloc and hipHostRegister)
+  std::map<uintptr_t, int> registered; // hipHostRegister base -> copies in flight
+  long n_registered = 0, n_refused = 0;  // hipHostRegister calls that pinned / were refused
   bool contains(const void* p, size_t n) {
     std::lock_guard<std::mutex> l(mu);
+    return base_of(p, n) != 0;
+  }
+  uintptr_t base_of(const void* p, size_t n) {  // mu held
     const uintptr_t a = (uintptr_t)p;
     auto it = blocks.upper_bound(a);
-    if (it == blocks.begin()) return false;
+    if (it == blocks.begin()) return 0;
     --it;
-    return a >= it->first && a + n <= it->first + it->second;
+    return a >= it->first && a + n <= it->first + it->second ? it->first : 0;
+  }
+  // a copy from / to registered memory starts (true) or ends: counted, so
+  // unregistering memory under a copy in flight is caught
+  void track(const void* p, size_t n, int d) {
+    std::lock_guard<std::mutex> l(mu);
+    const uintptr_t b = base_of(p, n);
+    auto it = registered.find(b);
+    if (it != registered.end()) it->second += d;
   }
 };
 inline Pinned& pinned() {
@@ -243,11 +261,50 @@ inline hipError_t hipStreamSynchronize(hipStream_t s) {
 inline hipError_t hipMemcpyAsync(void* dst, const void* src, size_t n, hipMemcpyKind kind,
                                  hipStream_t s) {
   fakehip::Stream* st = fake_stream(s);
-  const uint64_t t = st->push([dst, src, n] { std::memcpy(dst, src, n); });
-  // pageable host memory: the runtime's staged copy is done on return
   const void* host = kind == hipMemcpyHostToDevice ? src : kind == hipMemcpyDeviceToHost ? dst
                                                                                           : nullptr;
+  if (host) fakehip::pinned().track(host, n, +1);
+  const uint64_t t = st->push([dst, src, n, host] {
+    std::memcpy(dst, src, n);
+    if (host) fakehip::pinned().track(host, n, -1);
+  });
+  // pageable host memory: the runtime's staged copy is done on return
   if (host && !fakehip::pinned().contains(host, n)) st->wait(t);
+  return hipSuccess;
+}
+
+// Pins caller memory in place: copies to / from it become asynchronous like
+// any pinned copy.  Overlapping an existing pinned block is refused, as the
+// runtime refuses it; unregistering under a copy in flight aborts the test.
+inline hipError_t hipHostRegister(void* p, size_t n, unsigned) {
+  fakehip::Pinned& pn = fakehip::pinned();
+  std::lock_guard<std::mutex> l(pn.mu);
+  const uintptr_t a = (uintptr_t)p;
+  auto it = pn.blocks.upper_bound(a + n - 1);
+  if (it != pn.blocks.begin()) {
+    --it;
+    if (it->first + it->second > a) {
+      ++pn.n_refused;
+      return hipErrorHostMemoryAlreadyRegistered;
+    }
+  }
+  ++pn.n_registered;
+  pn.blocks[a] = n;
+  pn.registered[a] = 0;
+  return hipSuccess;
+}
+inline hipError_t hipHostUnregister(void* p) {
+  fakehip::Pinned& pn = fakehip::pinned();
+  std::lock_guard<std::mutex> l(pn.mu);
+  auto it = pn.registered.find((uintptr_t)p);
+  if (it == pn.registered.end()) return hipErrorHostMemoryNotRegistered;
+  if (it->second != 0) {
+    std::fprintf(stderr, "fake hip: hipHostUnregister(%p) with %d copies in flight\n", p,
+                 it->second);
+    std::abort();
+  }
+  pn.registered.erase(it);
+  pn.blocks.erase((uintptr_t)p);
   return hipSuccess;
 }
 

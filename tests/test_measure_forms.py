@@ -348,6 +348,34 @@ def test_host_staging_forms(gpu, le, oracle, staging, chunk_kib, measure):
         assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size)
 
 
+@pytest.mark.parametrize("pin_kib", ["0", "512", "5120"])
+def test_host_pinned_large_objects(gpu, le, oracle, pin_kib, measure):
+    """The measurement build's pinned form for large per-thread copies
+    (LEOEC_HOST_PIN=1, engine.cpp copy_large / pin_acquire): the caller's
+    memory above 1 MiB per segment is pinned in place and copied in pieces
+    of LEOEC_HOST_PIN_KIB (0: whole segments), then released.  Encode /
+    decode / repair of objects whose spans pass the 16 MiB zero-copy cap,
+    bit-exact with the oracle, and every registration released afterwards
+    (a second round over the same buffers pins them again)."""
+    measure.setenv("LEOEC_HOST_PIN", "1")
+    measure.setenv("LEOEC_HOST_PIN_KIB", pin_kib)
+    cases = [("vandrs", 10, 4, 8, (64 << 20) + 5), ("cauchyrs", 10, 4, 8, (17 << 20) + 77),
+             ("isars", 10, 4, 8, 20 << 20), ("liberation", 4, 2, 7, (17 << 20) + 1)]
+    for cls, k, m, w, size in cases:
+        data = rand_bytes(size, size + 17 * k)
+        ref = oracle.encode(cls, k, m, w, data)
+        for _ in range(2):
+            st, blocks = le.nif_encode(cls, (k, m, w), data, size)
+            assert st == "ok" and blocks == ref, (cls, k, m, w, size)
+            ids = list(range(m, k + m))[::-1]
+            st, out = le.nif_decode(cls, (k, m, w), [ref[b] for b in ids], ids, size)
+            assert st == "ok" and out == data, (cls, k, m, w, size)
+            lost = [0, k + m - 1]
+            avail = [b for b in range(k + m) if b not in lost]
+            st, rep = le.nif_repair(cls, (k, m, w), [ref[b] for b in avail], avail, lost)
+            assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size)
+
+
 @pytest.mark.parametrize("form", ["always-batch", "per-thread", "lanes4",
                                   "lanes4-always-batch", "fail-one", "zc-batch"])
 def test_host_batching_mixed_callers(gpu, le, oracle, form, measure):

@@ -1,0 +1,226 @@
+// capi_bench.cpp — measurement only: the host-memory C ABI (the NIF's entry
+// points) driven from plain C++ threads, with no Python and no torch in the
+// process, i.e. on the system HIP runtime (/opt/rocm) the library resolves
+// when an Erlang VM loads the NIF.  (Python tools run the engine on the HIP
+// runtime torch bundles, which is a different build: its pageable copies of
+// a 100 MiB object run ~5x faster than the system runtime's,
+// profiles/r04_s7_large_copy.log.)
+//
+//   g++ -O2 -std=c++17 -pthread -o tools/capi_bench tools/capi_bench.cpp -ldl
+//   tools/capi_bench <libleoec*.so> ref      [K=V,...]   the reference's eunit
+//                                                        encode benchmark (one
+//                                                        100 MiB zero object per
+//                                                        class; cold + warm calls)
+//   tools/capi_bench <libleoec*.so> callers  [K=V,...]   1 MiB RS(10,4,8) encode /
+//                                                        decode from 1, 8, 32 threads
+// K=V: measurement-build knobs (leoec_measure_set_knob), applied after load.
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+using GfInit = int (*)();
+using Layout = int (*)(int, int, int, int, uint64_t, uint64_t*, int*);
+using Encode = int (*)(int, int, int, int, const uint8_t*, uint64_t, uint8_t*, uint64_t);
+using Decode = int (*)(int, int, int, int, const uint8_t* const*, const int*, int, uint64_t,
+                       uint64_t, uint8_t*);
+using SetKnob = int (*)(const char*, const char*);
+
+GfInit gf_init;
+Layout layout;
+Encode encode;
+Decode decode;
+
+double now_s() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+void* sym(void* h, const char* name) {
+  void* p = dlsym(h, name);
+  if (!p) {
+    fprintf(stderr, "missing symbol %s\n", name);
+    exit(2);
+  }
+  return p;
+}
+
+// bench_encode_test (test/leo_erasure_tests.erl:207-212, 304-336): one encode
+// of a 100 MiB zero binary per class, rate = 100 / seconds.
+void ref_bench(int reps) {
+  struct Cls {
+    const char* name;
+    int id, k, m, w;
+  };
+  const Cls classes[] = {{"vandrs", 2, 10, 4, 8}, {"cauchyrs", 1, 10, 4, 10},
+                         {"liberation", 3, 10, 2, 11}, {"isars", 4, 10, 4, 8}};
+  const uint64_t size = 100ull << 20;
+  for (const Cls& c : classes) {
+    uint64_t bs;
+    int filled;
+    if (layout(c.id, c.k, c.m, c.w, size, &bs, &filled)) exit(3);
+    const uint64_t outn = (uint64_t)(c.k + c.m - filled) * bs;
+    std::vector<uint8_t> src(size, 0), out(outn, 0xA5);  // written: a fresh binary
+    auto call = [&] {
+      const double t0 = now_s();
+      const int rc = encode(c.id, c.k, c.m, c.w, src.data(), size, out.data(), outn);
+      const double dt = now_s() - t0;
+      if (rc) {
+        fprintf(stderr, "%s: rc %d\n", c.name, rc);
+        exit(4);
+      }
+      for (uint64_t i = 0; i < outn; i += 4093)
+        if (out[i]) {
+          fprintf(stderr, "%s: non-zero output\n", c.name);
+          exit(5);
+        }
+      return dt;
+    };
+    const double cold = call();
+    std::vector<double> warm;
+    for (int r = 0; r < reps; ++r) {
+      std::fill(out.begin(), out.end(), 0xA5);
+      warm.push_back(call());
+    }
+    std::sort(warm.begin(), warm.end());
+    const double med = warm[warm.size() / 2];
+    printf("{\"bench\": \"reference bench_encode_test, C ABI leoec_encode, 1 caller, system HIP "
+           "runtime\", \"class\": \"%s\", \"params\": [%d, %d, %d], \"cold_ms\": %.2f, "
+           "\"cold_MiBps\": %.1f, \"warm_ms\": %.2f, \"warm_MiBps\": %.1f, \"warm_min_ms\": %.2f}\n",
+           c.name, c.k, c.m, c.w, cold * 1e3, 100.0 / cold, med * 1e3, 100.0 / med,
+           warm[0] * 1e3);
+    fflush(stdout);
+  }
+}
+
+// tools/e2e_bench.py's callers(): T threads calling back to back, 1 MiB
+// RS(10,4,8) objects, 3 trials of 0.4 s after a warm-up trial, median.
+void callers(int T, bool dec) {
+  const int K = 10, M = 4, W = 8;
+  const uint64_t size = 1ull << 20;
+  uint64_t bs;
+  int filled;
+  if (layout(2, K, M, W, size, &bs, &filled)) exit(3);
+  const uint64_t outn = (uint64_t)(K + M - filled) * bs;
+  std::vector<std::vector<uint8_t>> srcs(T), outs(T), decs(T);
+  std::vector<std::vector<const uint8_t*>> ptrs(T);
+  std::vector<int> ids;
+  for (int i = 4; i < K + M; ++i) ids.push_back(i);
+  for (int t = 0; t < T; ++t) {
+    std::mt19937_64 g(t + 1);
+    srcs[t].resize(size);
+    for (auto& b : srcs[t]) b = (uint8_t)g();
+    outs[t].resize(outn);
+    decs[t].resize(size);
+    if (encode(2, K, M, W, srcs[t].data(), size, outs[t].data(), outn)) exit(4);
+    for (int i : ids)
+      ptrs[t].push_back(i < filled ? srcs[t].data() + (uint64_t)i * bs
+                                   : outs[t].data() + (uint64_t)(i - filled) * bs);
+  }
+  std::atomic<int> errs{0};
+  auto call = [&](int t) {
+    const int rc = dec ? decode(2, K, M, W, ptrs[t].data(), ids.data(), (int)ids.size(), bs, size,
+                                decs[t].data())
+                       : encode(2, K, M, W, srcs[t].data(), size, outs[t].data(), outn);
+    if (rc) errs++;
+  };
+  auto trial = [&](double per) {
+    std::vector<long> counts(T, 0);
+    std::atomic<int> ready{0};
+    std::atomic<bool> go{false};
+    double end = 0;
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        call(t);  // warm this thread outside the timed region
+        ready++;
+        while (!go.load()) std::this_thread::yield();
+        long n = 0;
+        while (now_s() < end) {
+          call(t);
+          ++n;
+        }
+        counts[t] = n;
+      });
+    while (ready.load() < T) std::this_thread::yield();
+    const double t0 = now_s();
+    end = t0 + per;
+    go = true;
+    for (auto& x : th) x.join();
+    const double dt = now_s() - t0;
+    long n = 0;
+    for (long c : counts) n += c;
+    return n * (double)size / dt / (double)(1ull << 30);
+  };
+  trial(0.4);
+  std::vector<double> r = {trial(0.4), trial(0.4), trial(0.4)};
+  std::sort(r.begin(), r.end());
+  if (dec)
+    for (int t = 0; t < T; ++t)
+      if (decs[t] != srcs[t]) {
+        fprintf(stderr, "decode mismatch\n");
+        exit(6);
+      }
+  printf("{\"path\": \"C ABI leoec_%s, 1 MiB objects, %d caller threads, system HIP runtime\", "
+         "\"GiBps\": %.2f, \"GiBps_min_max\": [%.2f, %.2f], \"errors\": %d}\n",
+         dec ? "decode" : "encode", T, r[1], r[0], r[2], errs.load());
+  fflush(stdout);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 3) {
+    fprintf(stderr, "usage: %s <libleoec*.so> ref|callers [K=V,...]\n", argv[0]);
+    return 2;
+  }
+  void* h = dlopen(argv[1], RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    fprintf(stderr, "%s\n", dlerror());
+    return 2;
+  }
+  gf_init = (GfInit)sym(h, "leoec_gf_init");
+  layout = (Layout)sym(h, "leoec_layout");
+  encode = (Encode)sym(h, "leoec_encode");
+  decode = (Decode)sym(h, "leoec_decode");
+  if (argc > 3 && argv[3][0]) {
+    auto set = (SetKnob)sym(h, "leoec_measure_set_knob");
+    std::string kv = argv[3];
+    size_t p = 0;
+    while (p < kv.size()) {
+      size_t q = kv.find(',', p);
+      if (q == std::string::npos) q = kv.size();
+      const std::string e = kv.substr(p, q - p);
+      const size_t eq = e.find('=');
+      if (eq != std::string::npos && set(e.substr(0, eq).c_str(), e.substr(eq + 1).c_str())) {
+        fprintf(stderr, "knob %s refused\n", e.c_str());
+        return 2;
+      }
+      p = q + 1;
+    }
+    printf("# knobs %s\n", argv[3]);
+  }
+  const double t0 = now_s();
+  const int rc = gf_init();
+  printf("{\"bench\": \"gf_init\", \"rc\": %d, \"ms\": %.2f}\n", rc, (now_s() - t0) * 1e3);
+  if (rc) return 3;
+  const std::string mode = argv[2];
+  if (mode == "ref") {
+    ref_bench(5);
+  } else {
+    for (bool dec : {false, true})
+      for (int T : {1, 8, 32}) callers(T, dec);
+  }
+  return 0;
+}

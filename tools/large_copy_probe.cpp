@@ -62,13 +62,30 @@ int main(int argc, char** argv) {
   uint8_t* dev;
   CHECK(hipMalloc(&dev, (size_t)(k + m) * bs));
   hipStream_t sa, sb;
-  CHECK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
-  CHECK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+  {  // the first stream of the process sets up the device's hardware queues
+    const double t0 = now_ms();
+    CHECK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+    const double t1 = now_ms();
+    CHECK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+    const double t2 = now_ms();
+    printf("{\"case\": \"hipStreamCreate\", \"first_ms\": %.3f, \"second_ms\": %.3f}\n", t1 - t0,
+           t2 - t1);
+  }
   std::vector<hipEvent_t> ev(64);
   for (auto& e : ev) CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   printf("# object %zu MiB, k %d m %d, bs %zu; host link bytes %zu\n", mib, k, m, bs,
          (size_t)k * bs + (size_t)m * bs);
 
+  {  // the first pageable copies of the process, and of these buffers
+    const double t0 = now_ms();
+    CHECK(hipMemcpy(dev, src, (size_t)k * bs, hipMemcpyHostToDevice));
+    const double t1 = now_ms();
+    CHECK(hipMemcpy(dev, src, (size_t)k * bs, hipMemcpyHostToDevice));
+    const double t2 = now_ms();
+    printf("{\"case\": \"pageable H2D of the object, first / second\", \"first_ms\": %.3f, "
+           "\"second_ms\": %.3f}\n", t1 - t0, t2 - t1);
+  }
+  const bool poison = argc > 3 && std::string(argv[3]) == "poison";
   auto reg = [&](bool on) {
     if (on) {
       CHECK(hipHostRegister(src, (size_t)k * bs, hipHostRegisterDefault));
@@ -114,12 +131,44 @@ int main(int argc, char** argv) {
     if (r) reg(false);
   };
 
+  if (poison) {
+    // do pageable async copies of memory that was registered and
+    // unregistered once read slower than before? (the same copies, timed
+    // before and after one hipHostRegister / hipHostUnregister of the
+    // buffers, and after it on a fresh buffer)
+    auto med3 = [&](const char* what) {
+      std::vector<double> v;
+      for (int r = 0; r < 5; ++r) {
+        const double t0 = now_ms();
+        serial(false);
+        v.push_back(now_ms() - t0);
+      }
+      std::sort(v.begin(), v.end());
+      printf("{\"case\": \"serial pageable async, %s\", \"ms_med\": %.3f, \"ms_min\": %.3f}\n",
+             what, v[2], v[0]);
+    };
+    med3("before any registration");
+    reg(true);
+    reg(false);
+    med3("after one register + unregister of these buffers");
+    uint8_t* src2 = static_cast<uint8_t*>(malloc((size_t)k * bs));
+    uint8_t* out2 = static_cast<uint8_t*>(malloc((size_t)m * bs));
+    memset(src2, 1, (size_t)k * bs);
+    memset(out2, 2, (size_t)m * bs);
+    std::swap(src, src2);
+    std::swap(out, out2);
+    med3("fresh buffers, never registered");
+    return 0;
+  }
   struct Case {
     std::string name;
     std::function<void()> fn;
   };
   std::vector<Case> cases = {{"serial", [&] { serial(false); }},
                              {"serial-reg", [&] { serial(true); }}};
+  for (int C : {1, 2}) {
+    cases.push_back({"chunk1d-reg-" + std::to_string(C), [&, C] { chunked(C, true, false); }});
+  }
   for (int C : {4, 8, 16}) {
     cases.push_back({"chunk2d-" + std::to_string(C), [&, C] { chunked(C, false, true); }});
     cases.push_back({"chunk2d-reg-" + std::to_string(C), [&, C] { chunked(C, true, true); }});
