@@ -471,6 +471,25 @@ constexpr int kStageSlots = 8;
 
 int hip_ok(hipError_t e) { return e == hipSuccess ? LEOEC_OK : LEOEC_E_HIP; }
 
+// Per-device pools of per-thread resources, filled by warm_device (gf_init)
+// so that a thread's first host call neither creates a stream (2-15 ms:
+// the first four streams of a process create the device's hardware queues,
+// profiles/r04_s11_streams.log) nor allocates its mapped zero-copy buffer;
+// a thread that exits gives them back.  Empty pools: created on demand.
+struct ResourcePool {
+  std::mutex mu;
+  std::vector<hipStream_t> streams;
+  struct Mapped {
+    uint8_t* h;
+    uint8_t* d;
+    size_t cap;
+  };
+  std::vector<Mapped> mapped;
+};
+ResourcePool g_pool[kMaxDevices];
+constexpr int kPoolStreams = 8;
+constexpr size_t kPoolMapped = (size_t)2 << 20;
+
 struct Staging {
   int device = -1;
   hipStream_t stream = nullptr;
@@ -509,8 +528,13 @@ struct Staging {
       if (buf) (void)hipFree(buf);
       if (ring) (void)hipHostFree(ring);
       if (hbuf) (void)hipHostFree(hbuf);
-      if (zh) (void)hipHostFree(zh);
-      (void)hipStreamDestroy(stream);
+      {  // the stream and a pool-sized mapped buffer go back to the pool
+        ResourcePool& p = g_pool[device];
+        std::lock_guard<std::mutex> l(p.mu);
+        p.streams.push_back(stream);
+        if (zh && zcap <= kPoolMapped) p.mapped.push_back(ResourcePool::Mapped{zh, zd, zcap});
+        else if (zh) (void)hipHostFree(zh);
+      }
     }
     device = -1;
     stream = nullptr;
@@ -605,7 +629,19 @@ bool zc_ready(Staging* st, size_t bytes) {
       st->zh = st->zd = nullptr;
       st->zcap = 0;
     }
-    const size_t want = std::max<size_t>(bytes + bytes / 4, (size_t)2 << 20);
+    if (bytes <= kPoolMapped) {  // a warmed-up buffer, if the pool has one
+      ResourcePool& p = g_pool[st->device];
+      std::lock_guard<std::mutex> l(p.mu);
+      if (!p.mapped.empty()) {
+        st->zh = p.mapped.back().h;
+        st->zd = p.mapped.back().d;
+        st->zcap = p.mapped.back().cap;
+        p.mapped.pop_back();
+      }
+    }
+  }
+  if (st->zcap < bytes) {
+    const size_t want = std::max<size_t>(bytes + bytes / 4, kPoolMapped);
     void* d = nullptr;
     if (hipHostMalloc((void**)&st->zh, want, hipHostMallocMapped) != hipSuccess) {
       st->zh = nullptr;
@@ -895,8 +931,18 @@ int get_staging(Staging** out) {
   if (dev < 0 || dev >= kMaxDevices) return LEOEC_E_NO_DEVICE;
   Staging& st = tl_staging[dev];
   if (st.device != dev) {
-    if (hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking) != hipSuccess)
+    {
+      ResourcePool& p = g_pool[dev];
+      std::lock_guard<std::mutex> l(p.mu);
+      if (!p.streams.empty()) {
+        st.stream = p.streams.back();
+        p.streams.pop_back();
+      }
+    }
+    if (!st.stream && hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking) != hipSuccess) {
+      st.stream = nullptr;
       return LEOEC_E_HIP;
+    }
     st.device = dev;
   }
   *out = &st;
@@ -1342,14 +1388,17 @@ int op_repair_dev(int coding, int k, int m, int w, const uint8_t* const* blocks,
 // staging stream, one small pageable copy each way, and one small launch
 // into every kernel code object of the library (gf8 for K = 1..16, the
 // packet-bitsliced kernel for w = 2..16, liberation / bitmatrix, w = 16/32)
-// on a scratch buffer.  Best effort: a failure here is not an error (each
-// call reports its own).
+// on a scratch buffer; then the resources other threads' first calls would
+// create (profiles/r04_s11_threads.log: 67 ms for the first 1 MiB call of a
+// second thread, 4.5 ms for each later one): the batching queue of the
+// device's lane, and pools of streams and mapped buffers.  Best effort: a
+// failure here is not an error (each call reports its own).
 int warm_device() {
   if (device_init() != LEOEC_OK) return LEOEC_OK;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return LEOEC_OK;
   static std::once_flag once[kMaxDevices];
-  std::call_once(once[dev], [] {
+  std::call_once(once[dev], [dev] {
     Staging* st;
     if (get_staging(&st)) return;
     constexpr size_t kScratch = 256u << 10, kPar = 128u << 10;
@@ -1372,6 +1421,25 @@ int warm_device() {
     }
     (void)hipStreamSynchronize(st->stream);
     (void)hipFree(d);
+    // the pools: streams and mapped buffers for the next calling threads
+    ResourcePool& p = g_pool[dev];
+    for (int i = 0; i < kPoolStreams; ++i) {
+      hipStream_t s = nullptr;
+      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) break;
+      uint8_t* h = nullptr;
+      void* dp = nullptr;
+      if (hipHostMalloc((void**)&h, kPoolMapped, hipHostMallocMapped) == hipSuccess) {
+        if (hipHostGetDevicePointer(&dp, h, 0) == hipSuccess) {
+          std::lock_guard<std::mutex> l(p.mu);
+          p.mapped.push_back(ResourcePool::Mapped{h, static_cast<uint8_t*>(dp), kPoolMapped});
+        } else {
+          (void)hipHostFree(h);
+        }
+      }
+      std::lock_guard<std::mutex> l(p.mu);
+      p.streams.push_back(s);
+    }
+    hostq_warm();  // the device's batching queue
   });
   return LEOEC_OK;
 }

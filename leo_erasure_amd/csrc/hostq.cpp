@@ -420,6 +420,12 @@ HostqTicket::~HostqTicket() {
 
 int hostq_lanes() { return device_init() == LEOEC_OK ? lane_count() : 0; }
 
+void hostq_warm() {
+  int lane = -1;
+  if (device_init() == LEOEC_OK && knobs().host_batch && pick_lane(&lane) == LEOEC_OK)
+    (void)queue_for(lane);
+}
+
 int hostq_spread(const int* devices, int n) {
   int rc = device_init();
   if (rc) return rc;

@@ -83,6 +83,11 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*) = 
 // without a device.
 int hostq_lanes();
 
+// gf_init's warm-up: creates the batching queue of the caller's current
+// device's lane now (its pinned arenas and threads: ~60 ms), rather than
+// inside the first batchable call.
+void hostq_warm();
+
 // leoec_host_spread: spread host-memory calls over these device ordinals
 // (n > 0), or run each on the caller's current device again (n == 0).
 // Returns the number of lanes in the set or a negative status.

@@ -78,7 +78,7 @@ const uint8_t* block(const Case& c, int id) { return c.ref.data() + (size_t)id *
 
 // encode, decode (m blocks lost, survivors listed in reverse), repair of two
 // blocks; t picks the erasure pattern
-void roundtrip(const Case& c, int t) {
+void roundtrip(const Case& c, int t, bool with_repair = true) {
   const int k = c.k, m = c.m, n = k + m;
   const uint64_t bs = c.bs;
   {
@@ -108,7 +108,7 @@ void roundtrip(const Case& c, int t) {
     if (rc || std::memcmp(out.data(), c.data.data(), c.size))
       fail("decode " + name(c) + " rc " + std::to_string(rc));
   }
-  {
+  if (with_repair) {
     const int rep[2] = {t % n, (t + 5) % n};
     const int nrep = rep[0] == rep[1] ? 1 : 2;
     std::vector<int> avail;
@@ -269,7 +269,8 @@ int main(int argc, char** argv) {
     Case large{LEOEC_VANDRS, 10, 4, 8, (17u << 20) + 5};
     prepare(&large, 12);
     std::vector<std::thread> th;
-    for (int t = 0; t < 3; ++t) th.emplace_back([&, t] { roundtrip(large, t); });
+    // (repair is left out: its span of k + 2 blocks stays under the cap)
+    for (int t = 0; t < 3; ++t) th.emplace_back([&, t] { roundtrip(large, t, false); });
     for (auto& x : th) x.join();
 #ifdef LEOEC_MEASURE
     leoec_measure_reset_knobs();

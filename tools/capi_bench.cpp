@@ -2,9 +2,8 @@
 // points) driven from plain C++ threads, with no Python and no torch in the
 // process, i.e. on the system HIP runtime (/opt/rocm) the library resolves
 // when an Erlang VM loads the NIF.  (Python tools run the engine on the HIP
-// runtime torch bundles, which is a different build: its pageable copies of
-// a 100 MiB object run ~5x faster than the system runtime's,
-// profiles/r04_s7_large_copy.log.)
+// runtime the torch wheel bundles, a different build; the two read the same
+// on these benchmarks, profiles/r04_s8_capi_*.log.)
 //
 //   g++ -O2 -std=c++17 -pthread -o tools/capi_bench tools/capi_bench.cpp -ldl
 //   tools/capi_bench <libleoec*.so> ref      [K=V,...]   the reference's eunit
@@ -13,6 +12,8 @@
 //                                                        class; cold + warm calls)
 //   tools/capi_bench <libleoec*.so> callers  [K=V,...]   1 MiB RS(10,4,8) encode /
 //                                                        decode from 1, 8, 32 threads
+//   tools/capi_bench <libleoec*.so> threads  [K=V,...]   first calls of new threads
+//                                                        after gf_init on the main one
 // K=V: measurement-build knobs (leoec_measure_set_knob), applied after load.
 #include <dlfcn.h>
 
@@ -178,6 +179,34 @@ void callers(int T, bool dec) {
   fflush(stdout);
 }
 
+// A VM calls gf_init on one thread and encodes on others (dirty
+// schedulers): the first call of each new thread, 1 MiB and 100 MiB.
+void new_threads() {
+  for (uint64_t size : {1ull << 20, 100ull << 20}) {
+    uint64_t bs;
+    int filled;
+    if (layout(2, 10, 4, 8, size, &bs, &filled)) exit(3);
+    const uint64_t outn = (uint64_t)(14 - filled) * bs;
+    std::vector<uint8_t> src(size, 0), out(outn, 0);
+    for (int i = 0; i < 3; ++i) {
+      double first = 0, second = 0;
+      std::thread t([&] {
+        double t0 = now_s();
+        if (encode(2, 10, 4, 8, src.data(), size, out.data(), outn)) exit(4);
+        first = now_s() - t0;
+        t0 = now_s();
+        if (encode(2, 10, 4, 8, src.data(), size, out.data(), outn)) exit(4);
+        second = now_s() - t0;
+      });
+      t.join();
+      printf("{\"bench\": \"first calls of a new thread after gf_init on another\", \"size\": %llu, "
+             "\"thread\": %d, \"first_ms\": %.3f, \"second_ms\": %.3f}\n",
+             (unsigned long long)size, i, first * 1e3, second * 1e3);
+      fflush(stdout);
+    }
+  }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -218,6 +247,8 @@ int main(int argc, char** argv) {
   const std::string mode = argv[2];
   if (mode == "ref") {
     ref_bench(5);
+  } else if (mode == "threads") {
+    new_threads();
   } else {
     for (bool dec : {false, true})
       for (int T : {1, 8, 32}) callers(T, dec);
