@@ -72,8 +72,10 @@ const char *leoec_strerror(int status);
 /* gf_init/0 (c_src/leo_erasure_nif.cpp:122-128): build the GF(2^8/16/32)
  * host tables, open the HIP device and warm the caller's current device once
  * (its hardware queues, the runtime's pageable-copy staging, every kernel
- * code object: ~0.1-0.2 s) so the first encode of the VM is not charged for
- * them.  Idempotent; other calls open the device lazily (without the warm-up). */
+ * code object, the device's batching queue, pools of streams and mapped
+ * buffers for other threads' first calls: 0.2-0.4 s) so the VM's first calls
+ * are not charged for them.  Idempotent; other calls open the device lazily
+ * (without the warm-up). */
 int leoec_gf_init(void);
 
 /* Coder::checkParams of the class (rscoding.cpp:29-34, cauchycoding.cpp:30-35,
