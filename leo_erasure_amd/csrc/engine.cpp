@@ -1007,10 +1007,78 @@ void pick_survivors(int coding, int k, const int* ids, const std::vector<int>& p
     if (present[id] >= 0) { surv->push_back(id); slot->push_back(present[id]); }
 }
 
+// A per-thread zero-copy call in column chunks (Knobs::zc_chunks).  A GF(2^w)
+// map is column-separable — output bytes [c0, c1) of every block depend
+// only on input bytes [c0, c1) — so the call packs chunk c's columns of
+// every input into the mapped buffer, launches the map on them, packs chunk
+// c + 1 while that launch reads chunk c over PCIe, and unpacks each chunk's
+// outputs once its launch is done (an event per chunk).  Inputs are placed
+// at base + i * stride, outputs at base + (nin + o) * stride.  Returns
+// kNotChunked when the call is not split (one chunk, a non-GF plan, blocks
+// too small): the caller then packs, launches and unpacks in one piece.
+struct ZcIn {
+  const uint8_t* host;
+  uint64_t valid;  // bytes of the block present (the rest reads as zero)
+};
+struct ZcOut {
+  uint8_t* host;
+  uint64_t n;  // bytes of the block to return
+};
+constexpr int kNotChunked = 1 << 20;
+constexpr uint64_t kZcChunkAlign = 4096;
+
+int zc_chunked(const Plan& plan, Staging* st, const std::vector<ZcIn>& in,
+               const std::vector<ZcOut>& out, uint64_t bs, uint64_t stride) {
+  const int want = std::min(knobs().zc_chunks, kStageSlots);
+  if (want <= 1 || plan.kind != Plan::kGf || !st->zc) return kNotChunked;
+  const uint64_t cw = round_to((bs + (uint64_t)want - 1) / (uint64_t)want, kZcChunkAlign);
+  if (cw >= bs) return kNotChunked;
+  const int nin = (int)in.size(), nout = (int)out.size();
+  int nc = 0;
+  for (uint64_t c0 = 0; c0 < bs; c0 += cw, ++nc) {
+    const uint64_t len = std::min(cw, bs - c0);
+    if (!st->ev[nc] && hipEventCreateWithFlags(&st->ev[nc], hipEventDisableTiming) != hipSuccess) {
+      st->ev[nc] = nullptr;
+      return LEOEC_E_HIP;
+    }
+    std::vector<Shard> si(nin), so(nout);
+    for (int i = 0; i < nin; ++i) {
+      const uint64_t v = in[i].valid > c0 ? std::min(in[i].valid - c0, len) : 0;
+      const uint64_t off = (uint64_t)i * stride + c0;
+      if (v) pack_pinned(st->zh + off, in[i].host + c0, (size_t)v, nin > 1);
+      si[i] = Shard{st->zd + off, 0, v};
+    }
+    for (int o = 0; o < nout; ++o) so[o] = Shard{st->zd + (uint64_t)(nin + o) * stride + c0, 0, len};
+    int rc = run_plan(plan, si, so, len, 1, st->stream);
+    if (rc == LEOEC_OK && hipEventRecord(st->ev[nc], st->stream) != hipSuccess) rc = LEOEC_E_HIP;
+    if (rc) {
+      (void)hipStreamSynchronize(st->stream);
+      return rc;
+    }
+  }
+  int c = 0;
+  for (uint64_t c0 = 0; c0 < bs; c0 += cw, ++c) {
+    const uint64_t len = std::min(cw, bs - c0);
+    if (hipEventSynchronize(st->ev[c]) != hipSuccess) {
+      (void)hipStreamSynchronize(st->stream);
+      return LEOEC_E_HIP;
+    }
+    for (int o = 0; o < nout; ++o) {
+      const uint64_t n = out[o].n > c0 ? std::min(out[o].n - c0, len) : 0;
+      if (n) std::memcpy(out[o].host + c0, st->zh + (uint64_t)(nin + o) * stride + c0, (size_t)n);
+    }
+  }
+  st->zc = false;
+  return LEOEC_OK;
+}
+
 // Stage the k survivor blocks, run the map into nwant device outputs (on the
-// calling thread's current device).
+// calling thread's current device).  With `zouts` (the host destinations of
+// the outputs) a zero-copy call may run in column chunks (zc_chunked), which
+// also returns the outputs: then *dev_out is nullptr.
 int run_host_map(const Plan& plan, const uint8_t* const* blocks, const std::vector<int>& slot,
-                 uint64_t bs, Staging** st_out, uint8_t** dev_out, uint64_t* stride_out) {
+                 uint64_t bs, Staging** st_out, uint8_t** dev_out, uint64_t* stride_out,
+                 const std::vector<ZcOut>* zouts = nullptr) {
   const Code& c = *plan.code;
   const std::vector<int>& want = plan.want;
   const int k = c.k;
@@ -1022,6 +1090,22 @@ int run_host_map(const Plan& plan, const uint8_t* const* blocks, const std::vect
   int rc = stage_for(span, &st, &zc);
   if (rc) return rc;
   uint8_t* base = zc ? st->zd : st->buf;
+  if (zc && zouts) {
+    std::vector<ZcIn> zi(k);
+    for (int i = 0; i < k; ++i) zi[i] = ZcIn{blocks[slot[i]], bs};
+    rc = zc_chunked(plan, st, zi, *zouts, bs16, bs16);
+    if (rc != kNotChunked) {
+      if (rc) {
+        st->zc = false;
+        return rc;
+      }
+      *st_out = st;
+      *dev_out = nullptr;
+      *stride_out = bs16;
+      return LEOEC_OK;
+    }
+    rc = LEOEC_OK;
+  }
   std::vector<Shard> in(k), out(want.size());
   std::vector<H2DSeg> segs(k);
   for (int i = 0; i < k; ++i) {
@@ -1132,6 +1216,19 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
   rc = stage_for((size_t)(k + m) * bs, &st, &zc);
   if (rc) return rc;
   uint8_t* base = zc ? st->zd : st->buf;
+  if (zc) {  // column chunks, when Knobs::zc_chunks asks for them
+    std::vector<ZcIn> zi(k);
+    std::vector<ZcOut> zo(m);
+    for (int j = 0; j < k; ++j)
+      zi[j] = ZcIn{obj + (uint64_t)j * bs, clamp_valid(size, (uint64_t)j * bs, bs)};
+    for (int i = 0; i < m; ++i) zo[i] = ZcOut{out + tail_bytes + (uint64_t)i * bs, bs};
+    rc = zc_chunked(*plan, st, zi, zo, bs, bs);
+    if (rc != kNotChunked) {
+      if (rc) st->zc = false;
+      return rc;
+    }
+    rc = LEOEC_OK;
+  }
   std::vector<Shard> in(k), par(m);
   for (int j = 0; j < k; ++j)
     in[j] = Shard{base + (uint64_t)j * bs, 0, clamp_valid(size, (uint64_t)j * bs, bs)};
@@ -1216,11 +1313,14 @@ int op_decode(int coding, int k, int m, int w, const uint8_t* const* blocks, con
     if (where == 0) survivors.done = true;
     on.reset(new DeviceScope(ticket.device));
     if (!on->ok()) return LEOEC_E_HIP;
-    rc = run_host_map(*plan, blocks, slot, bs, &st, &dev, &dstride);
+    std::vector<ZcOut> zo;
+    for (size_t o = 0; o < want.size(); ++o)
+      zo.push_back(ZcOut{out + (uint64_t)want[o] * bs, clamp_valid(size, (uint64_t)want[o] * bs, bs)});
+    rc = run_host_map(*plan, blocks, slot, bs, &st, &dev, &dstride, &zo);
     if (rc) return rc;
   }
   if (!survivors.done) Survivors::copy(&survivors);
-  if (!st) return LEOEC_OK;
+  if (!st || !dev) return LEOEC_OK;  // no map, or the chunked form returned its outputs
   std::vector<D2HSeg> segs;
   for (size_t o = 0; o < want.size(); ++o) {
     const uint64_t off = (uint64_t)want[o] * bs;
@@ -1277,8 +1377,10 @@ int op_repair(int coding, int k, int m, int w, const uint8_t* const* blocks, con
   Staging* st;
   uint8_t* dev;
   uint64_t dstride;
-  rc = run_host_map(*plan, blocks, slot, bs, &st, &dev, &dstride);
-  if (rc) return rc;
+  std::vector<ZcOut> zo;
+  for (size_t o = 0; o < want.size(); ++o) zo.push_back(ZcOut{out + (uint64_t)pos[o] * bs, bs});
+  rc = run_host_map(*plan, blocks, slot, bs, &st, &dev, &dstride, &zo);
+  if (rc || !dev) return rc;  // !dev: the chunked form returned the outputs
   std::vector<D2HSeg> segs;
   for (size_t o = 0; o < want.size(); ++o)
     segs.push_back(D2HSeg{out + (uint64_t)pos[o] * bs, dev + o * dstride, (size_t)bs});

@@ -348,6 +348,36 @@ def test_host_staging_forms(gpu, le, oracle, staging, chunk_kib, measure):
         assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size)
 
 
+@pytest.mark.parametrize("chunks", ["2", "3", "8"])
+def test_host_zero_copy_chunks(gpu, le, oracle, chunks, measure):
+    """The measurement build's chunked zero-copy form (LEOEC_ZC_CHUNKS,
+    engine.cpp zc_chunked): a lone caller's GF(2^w) map in column chunks,
+    packing chunk c + 1 while chunk c runs and unpacking each as its launch
+    completes.  Encode / decode / repair through the per-thread path (the
+    queue never batches: LEOEC_HOST_BATCH=0), bit-exact with the oracle, over
+    ragged sizes and chunk edges inside and past the valid bytes; bitmatrix
+    classes fall back to one piece."""
+    measure.setenv("LEOEC_ZC_CHUNKS", chunks)
+    measure.setenv("LEOEC_HOST_BATCH", "0")
+    cases = [("vandrs", 10, 4, 8, 1 << 20), ("vandrs", 10, 4, 8, (1 << 20) - 4095),
+             ("isars", 10, 4, 8, 3 * (1 << 20) + 17), ("vandrs", 4, 2, 8, 40000),
+             ("vandrs", 6, 3, 16, 777777), ("vandrs", 5, 3, 32, 1 << 20),
+             ("vandrs", 20, 6, 8, 2000003), ("cauchyrs", 10, 4, 8, 1 << 20),
+             ("liberation", 7, 2, 7, 1 << 20)]
+    for cls, k, m, w, size in cases:
+        data = rand_bytes(size, size + 31 * k)
+        ref = oracle.encode(cls, k, m, w, data)
+        st, blocks = le.nif_encode(cls, (k, m, w), data, size)
+        assert st == "ok" and blocks == ref, (cls, k, m, w, size)
+        ids = list(range(m, k + m))[::-1]
+        st, out = le.nif_decode(cls, (k, m, w), [ref[b] for b in ids], ids, size)
+        assert st == "ok" and out == data, (cls, k, m, w, size)
+        lost = [0, k + m - 1]
+        avail = [b for b in range(k + m) if b not in lost]
+        st, rep = le.nif_repair(cls, (k, m, w), [ref[b] for b in avail], avail, lost)
+        assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size)
+
+
 @pytest.mark.parametrize("pin_kib", ["0", "512", "5120"])
 def test_host_pinned_large_objects(gpu, le, oracle, pin_kib, measure):
     """The measurement build's pinned form for large per-thread copies

@@ -207,6 +207,44 @@ void new_threads() {
   }
 }
 
+// One thread, back-to-back 1 MiB RS(10,4,8) encodes (a short target for a
+// kernel / API trace of the lone-caller path): `n` calls, mean per call.
+void lone(int n) {
+  const uint64_t size = 1ull << 20;
+  uint64_t bs;
+  int filled;
+  if (layout(2, 10, 4, 8, size, &bs, &filled)) exit(3);
+  const uint64_t outn = (uint64_t)(14 - filled) * bs;
+  std::vector<uint8_t> src(size, 7), out(outn, 0);
+  for (int i = 0; i < 50; ++i)
+    if (encode(2, 10, 4, 8, src.data(), size, out.data(), outn)) exit(4);
+  const double t0 = now_s();
+  for (int i = 0; i < n; ++i)
+    if (encode(2, 10, 4, 8, src.data(), size, out.data(), outn)) exit(4);
+  const double dt = now_s() - t0;
+  printf("{\"bench\": \"lone caller, 1 MiB encodes back to back\", \"calls\": %d, "
+         "\"us_per_call\": %.2f, \"GiBps\": %.2f}\n",
+         n, dt / n * 1e6, n * (double)size / dt / (double)(1ull << 30));
+  // decodes of data blocks 0-3 from blocks 4..13
+  std::vector<int> ids;
+  std::vector<const uint8_t*> ptrs;
+  for (int i = 4; i < 14; ++i) {
+    ids.push_back(i);
+    ptrs.push_back(i < filled ? src.data() + (uint64_t)i * bs : out.data() + (uint64_t)(i - filled) * bs);
+  }
+  std::vector<uint8_t> dec(size);
+  for (int i = 0; i < 50; ++i)
+    if (decode(2, 10, 4, 8, ptrs.data(), ids.data(), 10, bs, size, dec.data())) exit(4);
+  const double t1 = now_s();
+  for (int i = 0; i < n; ++i)
+    if (decode(2, 10, 4, 8, ptrs.data(), ids.data(), 10, bs, size, dec.data())) exit(4);
+  const double dt2 = now_s() - t1;
+  if (dec != src) exit(6);
+  printf("{\"bench\": \"lone caller, 1 MiB decodes (lose 0-3) back to back\", \"calls\": %d, "
+         "\"us_per_call\": %.2f, \"GiBps\": %.2f}\n",
+         n, dt2 / n * 1e6, n * (double)size / dt2 / (double)(1ull << 30));
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -249,6 +287,8 @@ int main(int argc, char** argv) {
     ref_bench(5);
   } else if (mode == "threads") {
     new_threads();
+  } else if (mode == "lone") {
+    lone(2000);
   } else {
     for (bool dec : {false, true})
       for (int T : {1, 8, 32}) callers(T, dec);
