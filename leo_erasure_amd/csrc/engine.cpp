@@ -1012,8 +1012,9 @@ void pick_survivors(int coding, int k, const int* ids, const std::vector<int>& p
 // only on input bytes [c0, c1) — so the call packs chunk c's columns of
 // every input into the mapped buffer, launches the map on them, packs chunk
 // c + 1 while that launch reads chunk c over PCIe, and unpacks each chunk's
-// outputs once its launch is done (an event per chunk).  Inputs are placed
-// at base + i * stride, outputs at base + (nin + o) * stride.  Returns
+// outputs once its launch is done (an event per chunk); `overlap` runs
+// between the last launch and the first wait.  Inputs are placed at
+// base + i * stride, outputs at base + (nin + o) * stride.  Returns
 // kNotChunked when the call is not split (one chunk, a non-GF plan, blocks
 // too small): the caller then packs, launches and unpacks in one piece.
 struct ZcIn {
@@ -1028,7 +1029,8 @@ constexpr int kNotChunked = 1 << 20;
 constexpr uint64_t kZcChunkAlign = 4096;
 
 int zc_chunked(const Plan& plan, Staging* st, const std::vector<ZcIn>& in,
-               const std::vector<ZcOut>& out, uint64_t bs, uint64_t stride) {
+               const std::vector<ZcOut>& out, uint64_t bs, uint64_t stride,
+               void (*overlap)(void*) = nullptr, void* arg = nullptr) {
   const int want = std::min(knobs().zc_chunks, kStageSlots);
   if (want <= 1 || plan.kind != Plan::kGf || !st->zc) return kNotChunked;
   const uint64_t cw = round_to((bs + (uint64_t)want - 1) / (uint64_t)want, kZcChunkAlign);
@@ -1056,6 +1058,7 @@ int zc_chunked(const Plan& plan, Staging* st, const std::vector<ZcIn>& in,
       return rc;
     }
   }
+  if (overlap) overlap(arg);  // the caller's own host copies, while the chunks run
   int c = 0;
   for (uint64_t c0 = 0; c0 < bs; c0 += cw, ++c) {
     const uint64_t len = std::min(cw, bs - c0);
@@ -1075,10 +1078,12 @@ int zc_chunked(const Plan& plan, Staging* st, const std::vector<ZcIn>& in,
 // Stage the k survivor blocks, run the map into nwant device outputs (on the
 // calling thread's current device).  With `zouts` (the host destinations of
 // the outputs) a zero-copy call may run in column chunks (zc_chunked), which
-// also returns the outputs: then *dev_out is nullptr.
+// also returns the outputs and runs `overlap` while the chunks are on the
+// GPU: then *dev_out is nullptr.
 int run_host_map(const Plan& plan, const uint8_t* const* blocks, const std::vector<int>& slot,
                  uint64_t bs, Staging** st_out, uint8_t** dev_out, uint64_t* stride_out,
-                 const std::vector<ZcOut>* zouts = nullptr) {
+                 const std::vector<ZcOut>* zouts = nullptr, void (*overlap)(void*) = nullptr,
+                 void* arg = nullptr) {
   const Code& c = *plan.code;
   const std::vector<int>& want = plan.want;
   const int k = c.k;
@@ -1093,7 +1098,7 @@ int run_host_map(const Plan& plan, const uint8_t* const* blocks, const std::vect
   if (zc && zouts) {
     std::vector<ZcIn> zi(k);
     for (int i = 0; i < k; ++i) zi[i] = ZcIn{blocks[slot[i]], bs};
-    rc = zc_chunked(plan, st, zi, *zouts, bs16, bs16);
+    rc = zc_chunked(plan, st, zi, *zouts, bs16, bs16, overlap, arg);
     if (rc != kNotChunked) {
       if (rc) {
         st->zc = false;
@@ -1316,8 +1321,10 @@ int op_decode(int coding, int k, int m, int w, const uint8_t* const* blocks, con
     std::vector<ZcOut> zo;
     for (size_t o = 0; o < want.size(); ++o)
       zo.push_back(ZcOut{out + (uint64_t)want[o] * bs, clamp_valid(size, (uint64_t)want[o] * bs, bs)});
-    rc = run_host_map(*plan, blocks, slot, bs, &st, &dev, &dstride, &zo);
+    rc = run_host_map(*plan, blocks, slot, bs, &st, &dev, &dstride, &zo,
+                      survivors.done ? nullptr : &Survivors::copy, &survivors);
     if (rc) return rc;
+    if (!dev) survivors.done = true;  // the chunked form ran the copy
   }
   if (!survivors.done) Survivors::copy(&survivors);
   if (!st || !dev) return LEOEC_OK;  // no map, or the chunked form returned its outputs

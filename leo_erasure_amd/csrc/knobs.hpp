@@ -22,9 +22,11 @@ struct Knobs {
                              //   refcounted) and copies it in pieces of LEOEC_HOST_PIN_KIB
                              //   (0: one copy per segment) instead of a pageable copy
   int host_pin_kib = 0;
-  int zc_chunks = 1;         // LEOEC_ZC_CHUNKS: a per-thread zero-copy call of a GF(2^w) map
+  int zc_chunks = 2;         // LEOEC_ZC_CHUNKS: a per-thread zero-copy call of a GF(2^w) map
                              //   in this many column chunks, packing chunk c + 1 while
                              //   chunk c's launch runs and unpacking each as it completes
+                             //   (shipped at 2 since round 4: a lone 1 MiB encode 79.6 ->
+                             //   70.2 us, profiles/r04_s14_lone_*.log; 3 and 4 lose)
   int host_batch = 1;        // LEOEC_HOST_BATCH=0: host calls take the per-thread path only
   int batch_window_us = 0;   // LEOEC_BATCH_WINDOW_US: hold an idle-GPU batch open this long
   int hostq_depth = 3;       // LEOEC_HOSTQ_DEPTH: batches on the GPU at once
