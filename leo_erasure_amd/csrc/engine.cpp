@@ -1014,9 +1014,9 @@ void pick_survivors(int coding, int k, const int* ids, const std::vector<int>& p
 // c + 1 while that launch reads chunk c over PCIe, and unpacks each chunk's
 // outputs once its launch is done (an event per chunk); `overlap` runs
 // between the last launch and the first wait.  Inputs are placed at
-// base + i * stride, outputs at base + (nin + o) * stride.  Returns
-// kNotChunked when the call is not split (one chunk, a non-GF plan, blocks
-// too small): the caller then packs, launches and unpacks in one piece.
+// base + i * stride, outputs at base + (nin + o) * stride.  *ran is false
+// when the call is not split (one chunk, a non-GF plan, blocks too small):
+// the caller then packs, launches and unpacks in one piece.
 struct ZcIn {
   const uint8_t* host;
   uint64_t valid;  // bytes of the block present (the rest reads as zero)
@@ -1025,16 +1025,17 @@ struct ZcOut {
   uint8_t* host;
   uint64_t n;  // bytes of the block to return
 };
-constexpr int kNotChunked = 1 << 20;
 constexpr uint64_t kZcChunkAlign = 4096;
 
 int zc_chunked(const Plan& plan, Staging* st, const std::vector<ZcIn>& in,
-               const std::vector<ZcOut>& out, uint64_t bs, uint64_t stride,
+               const std::vector<ZcOut>& out, uint64_t bs, uint64_t stride, bool* ran,
                void (*overlap)(void*) = nullptr, void* arg = nullptr) {
+  *ran = false;
   const int want = std::min(knobs().zc_chunks, kStageSlots);
-  if (want <= 1 || plan.kind != Plan::kGf || !st->zc) return kNotChunked;
+  if (want <= 1 || plan.kind != Plan::kGf || !st->zc) return LEOEC_OK;
   const uint64_t cw = round_to((bs + (uint64_t)want - 1) / (uint64_t)want, kZcChunkAlign);
-  if (cw >= bs) return kNotChunked;
+  if (cw >= bs) return LEOEC_OK;
+  *ran = true;
   const int nin = (int)in.size(), nout = (int)out.size();
   int nc = 0;
   for (uint64_t c0 = 0; c0 < bs; c0 += cw, ++nc) {
@@ -1098,18 +1099,18 @@ int run_host_map(const Plan& plan, const uint8_t* const* blocks, const std::vect
   if (zc && zouts) {
     std::vector<ZcIn> zi(k);
     for (int i = 0; i < k; ++i) zi[i] = ZcIn{blocks[slot[i]], bs};
-    rc = zc_chunked(plan, st, zi, *zouts, bs16, bs16, overlap, arg);
-    if (rc != kNotChunked) {
-      if (rc) {
-        st->zc = false;
-        return rc;
-      }
+    bool ran;
+    rc = zc_chunked(plan, st, zi, *zouts, bs16, bs16, &ran, overlap, arg);
+    if (rc) {
+      st->zc = false;
+      return rc;
+    }
+    if (ran) {
       *st_out = st;
       *dev_out = nullptr;
       *stride_out = bs16;
       return LEOEC_OK;
     }
-    rc = LEOEC_OK;
   }
   std::vector<Shard> in(k), out(want.size());
   std::vector<H2DSeg> segs(k);
@@ -1227,12 +1228,10 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
     for (int j = 0; j < k; ++j)
       zi[j] = ZcIn{obj + (uint64_t)j * bs, clamp_valid(size, (uint64_t)j * bs, bs)};
     for (int i = 0; i < m; ++i) zo[i] = ZcOut{out + tail_bytes + (uint64_t)i * bs, bs};
-    rc = zc_chunked(*plan, st, zi, zo, bs, bs);
-    if (rc != kNotChunked) {
-      if (rc) st->zc = false;
-      return rc;
-    }
-    rc = LEOEC_OK;
+    bool ran;
+    rc = zc_chunked(*plan, st, zi, zo, bs, bs, &ran);
+    if (rc) st->zc = false;
+    if (rc || ran) return rc;
   }
   std::vector<Shard> in(k), par(m);
   for (int j = 0; j < k; ++j)
