@@ -169,8 +169,11 @@ int leoec_host_lanes(int *devices, int cap);
  * current device is left as it was; n == 0 restores the default (the
  * caller's current device).  Every ordinal must be a gfx950 device visible
  * to the process (else LEOEC_E_NO_DEVICE, and the setting is unchanged).
- * Returns the number of devices in the set.  Only the devices used get
- * queues and pinned arenas (5 x 32 MiB pinned + 5 x 32 MiB device each).
+ * Returns the number of devices in the set.  Only the devices of the set get
+ * queues and pinned arenas (5 x 32 MiB pinned + 5 x 32 MiB device each), and
+ * each of them is warmed before this returns, as gf_init warms the caller's
+ * device (its hardware queues, code objects, batching queue and pools, one
+ * thread per device: ~0.3 s once), so no device's first call pays that.
  * (No reference counterpart: the reference is CPU-only.) */
 int leoec_host_spread(const int *devices, int n);
 

@@ -92,6 +92,9 @@ def _load(path=LIB_PATH):
         L.leoec_measure_set_knob.restype = ctypes.c_int
         L.leoec_measure_reset_knobs.argtypes = []
         L.leoec_measure_reset_knobs.restype = None
+    if hasattr(L, "leoec_measure_warm_state"):
+        L.leoec_measure_warm_state.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        L.leoec_measure_warm_state.restype = None
     if hasattr(L, "leoec_measure_xor_pattern_dev"):  # measurement build (xor_pattern.hip)
         L.leoec_measure_xor_pattern_dev.argtypes = [
             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
@@ -161,6 +164,17 @@ def measure_set_knob(name, value):
                                          None if value is None else str(value).encode())
     if rc != 0:
         raise ValueError(f"not a knob: {name}")
+
+
+def measure_warm_state(dev):
+    """Measurement build only: what the warm-up left on device `dev`:
+    {pool_streams, pool_mapped, queue (every lane of the device has its
+    batching queue), queues_built (by the process)}."""
+    _need_measure()
+    out = (ctypes.c_int * 4)()
+    _current.leoec_measure_warm_state(dev, out)
+    return {"pool_streams": out[0], "pool_mapped": out[1], "queue": bool(out[2]),
+            "queues_built": out[3]}
 
 
 def measure_reset_knobs():

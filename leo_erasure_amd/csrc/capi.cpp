@@ -59,7 +59,7 @@ int leoec_gf_init(void) {
   return guarded([] {
     for (int w : {8, 16, 32}) (void)leoec::field(w);
     const int rc = leoec::device_init();
-    if (rc == LEOEC_OK) (void)leoec::warm_device();
+    if (rc == LEOEC_OK) (void)leoec::warm_current_device();
     return rc;
   });
 }
@@ -163,8 +163,15 @@ int leoec_host_lanes(int* devices, int cap) {
   });
 }
 
+// The set's devices are warmed before this returns (engine.cpp
+// warm_devices): a device's first call then neither creates its hardware
+// queues nor its lane's batching queue behind the callers.
 int leoec_host_spread(const int* devices, int n) {
-  return guarded([&] { return leoec::hostq_spread(devices, n); });
+  return guarded([&] {
+    const int rc = leoec::hostq_spread(devices, n);
+    if (rc > 0) leoec::warm_devices(devices, n);
+    return rc;
+  });
 }
 
 const char* leoec_version(void) { return LEOEC_VERSION " (gfx950)"; }

@@ -102,9 +102,25 @@ int op_repair_dev(int coding, int k, int m, int w, const uint8_t* const* blocks,
                   uint64_t block_stride, uint64_t bs, uint64_t nobj, const int* rep, int nrep,
                   uint8_t* const* out, uint64_t out_stride, hipStream_t s);
 
-// gf_init's runtime warm-up on the caller's current device (once per
-// device; best effort, always LEOEC_OK): hardware queues, the pageable-copy
-// staging, every kernel code object.
-int warm_device();
+// The runtime warm-up of one device (once per device; best effort, always
+// LEOEC_OK): hardware queues, the pageable-copy staging, every kernel code
+// object, the device's batching queue and its pools of per-thread streams
+// and mapped buffers.  gf_init warms the caller's current device;
+// leoec_host_spread warms every device of its set (warm_devices, one thread
+// per device).
+int warm_device(int dev);
+int warm_current_device();
+void warm_devices(const int* devs, int n);
+
+// What the warm-up left on a device (tests): pooled streams and mapped
+// buffers not yet taken by a thread, whether every lane of the device has
+// its batching queue, and the process's count of built queues.
+struct WarmState {
+  int pool_streams = 0;
+  int pool_mapped = 0;
+  bool queue = false;
+  int queues_built = 0;
+};
+WarmState warm_state(int dev);
 
 }  // namespace leoec

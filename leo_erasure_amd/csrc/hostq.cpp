@@ -374,37 +374,54 @@ int pick_lane(int* lane) {
   return LEOEC_E_NO_DEVICE;
 }
 
-Queue* queue_for(int lane) {
-  static std::mutex mu;
-  static Queue* queues[kMaxLanes] = {};
-  static bool failed[kMaxLanes] = {};
-  if (lane < 0 || lane >= kMaxLanes) return nullptr;
-  std::lock_guard<std::mutex> lock(mu);
-  if (!queues[lane] && !failed[lane]) {
-    // every slot's buffers up front, each touched once by a copy each way:
-    // the first transfer through a new pinned buffer costs milliseconds,
-    // which a caller should not pay inside the queue's lock
-    const int dev = lane_device(lane);
-    DeviceScope on(dev);
-    Queue* q = new Queue;
-    q->device = dev;
-    for (Slot& sl : q->slots) {
-      sl.lane = lane;
-      if (!on.ok() || slot_alloc(&sl) != LEOEC_OK ||
-          hipMemcpyAsync(sl.d_in, sl.h_in, kSlotBytes, hipMemcpyHostToDevice, sl.stream) !=
-              hipSuccess ||
-          hipMemcpyAsync(sl.h_out, sl.d_out, kSlotBytes, hipMemcpyDeviceToHost, sl.stream) !=
-              hipSuccess ||
-          hipStreamSynchronize(sl.stream) != hipSuccess) {
-        failed[lane] = true;  // no batching on this lane (pinned memory short): per-thread path
-        return nullptr;       // (the partial queue is leaked, as queues are)
-      }
-    }
-    std::thread(worker_main, q).detach();
-    std::thread(completer_main, q).detach();
-    queues[lane] = q;
+// Build lane `lane`'s queue: every slot's buffers up front, each touched once
+// by a copy each way (the first transfer through a new pinned buffer costs
+// milliseconds, which a caller should not pay inside the queue's lock).
+// nullptr when pinned or device memory is short (the lane then has no
+// batching: its calls take the per-thread path; the partial queue is
+// leaked, as queues are).
+Queue* build_queue(int lane) {
+  const int dev = lane_device(lane);
+  DeviceScope on(dev);
+  if (!on.ok()) return nullptr;
+  Queue* q = new Queue;
+  q->device = dev;
+  for (Slot& sl : q->slots) {
+    sl.lane = lane;
+    if (slot_alloc(&sl) != LEOEC_OK ||
+        hipMemcpyAsync(sl.d_in, sl.h_in, kSlotBytes, hipMemcpyHostToDevice, sl.stream) !=
+            hipSuccess ||
+        hipMemcpyAsync(sl.h_out, sl.d_out, kSlotBytes, hipMemcpyDeviceToHost, sl.stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(sl.stream) != hipSuccess)
+      return nullptr;
   }
-  return queues[lane];
+  std::thread(worker_main, q).detach();
+  std::thread(completer_main, q).detach();
+  return q;
+}
+
+// One queue per lane, built once (~60 ms: 5 x 32 MiB of pinned arenas and
+// their device twins) under the lane's own once_flag, so lanes of different
+// devices are built concurrently (gf_init / leoec_host_spread warm several
+// devices at once) and a caller waits only for the lane it needs.
+struct LaneQueue {
+  std::once_flag once;
+  std::atomic<Queue*> q{nullptr};
+};
+LaneQueue g_lane_queue[kMaxLanes];
+std::atomic<int> g_queues_built{0};
+
+Queue* queue_for(int lane) {
+  if (lane < 0 || lane >= kMaxLanes) return nullptr;
+  LaneQueue& L = g_lane_queue[lane];
+  std::call_once(L.once, [&L, lane] {
+    if (Queue* q = build_queue(lane)) {
+      L.q.store(q, std::memory_order_release);
+      g_queues_built.fetch_add(1, std::memory_order_relaxed);
+    }
+  });
+  return L.q.load(std::memory_order_acquire);
 }
 
 }  // namespace
@@ -420,11 +437,26 @@ HostqTicket::~HostqTicket() {
 
 int hostq_lanes() { return device_init() == LEOEC_OK ? lane_count() : 0; }
 
-void hostq_warm() {
-  int lane = -1;
-  if (device_init() == LEOEC_OK && knobs().host_batch && pick_lane(&lane) == LEOEC_OK)
-    (void)queue_for(lane);
+void hostq_warm(int dev) {
+  if (device_init() != LEOEC_OK || !knobs().host_batch) return;
+  const int n = lane_count();
+  for (int l = 0; l < n; ++l)
+    if (lane_device(l) == dev) (void)queue_for(l);
 }
+
+bool hostq_queue_ready(int dev) {
+  if (device_init() != LEOEC_OK) return false;
+  const int n = lane_count();
+  bool any = false;
+  for (int l = 0; l < n; ++l)
+    if (lane_device(l) == dev) {
+      if (!g_lane_queue[l].q.load(std::memory_order_acquire)) return false;
+      any = true;
+    }
+  return any;
+}
+
+int hostq_queues_built() { return g_queues_built.load(std::memory_order_relaxed); }
 
 int hostq_spread(const int* devices, int n) {
   int rc = device_init();

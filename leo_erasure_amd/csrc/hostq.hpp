@@ -83,10 +83,15 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*) = 
 // without a device.
 int hostq_lanes();
 
-// gf_init's warm-up: creates the batching queue of the caller's current
-// device's lane now (its pinned arenas and threads: ~60 ms), rather than
-// inside the first batchable call.
-void hostq_warm();
+// Warm-up (gf_init, leoec_host_spread): creates the batching queue of every
+// lane on device `dev` now (its pinned arenas and threads: ~60 ms), rather
+// than inside the first batchable call.
+void hostq_warm(int dev);
+
+// Whether every lane of device `dev` has its queue (tests: the warm-up made
+// them), and how many queues this process has built.
+bool hostq_queue_ready(int dev);
+int hostq_queues_built();
 
 // leoec_host_spread: spread host-memory calls over these device ordinals
 // (n > 0), or run each on the caller's current device again (n == 0).

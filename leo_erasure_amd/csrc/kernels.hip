@@ -179,9 +179,26 @@ LibFn lib_kernel(int w) {
   }
 }
 
-int launch_lib(const BitApply& p, LibFn fn, hipStream_t s) {
+// Knobs::lib_buf: the branch-free forms (libb_apply / libb_dec_apply,
+// lib_inst.hip), look-ahead lib_la / lib_dec_la and lib_wg / lib_dec_wg
+// lanes in the measurement build (the shipped form when that one is not
+// built).
+LibbEnc libb_enc(int w, int k) {
+  const Knobs& kn = knobs();
+  const int la = kMeasureBuild ? kn.lib_la : kLibbEncLA;
+  const int tw = kMeasureBuild ? kn.lib_wg : kLibbEncTW;
+  switch (w) {
+    case 3: return libb_enc_pick<3>(k, la, tw);
+    case 5: return libb_enc_pick<5>(k, la, tw);
+    case 7: return libb_enc_pick<7>(k, la, tw);
+    case 11: return libb_enc_pick<11>(k, la, tw);
+    case 13: return libb_enc_pick<13>(k, la, tw);
+    default: return {nullptr, 0};
+  }
+}
+
+int launch_lib(const BitApply& p, LibFn fn, uint32_t lanes, hipStream_t s) {
   const uint32_t ps = (uint32_t)(p.block_size / (uint64_t)p.w);
-  const uint32_t lanes = lib_lanes();
   const uint32_t tb = lanes * 16u;
   const uint32_t tiles = (ps + tb - 1) / tb;
   const uint64_t max_obj = (uint64_t)0x7FFFFFFF / tiles;
@@ -290,6 +307,19 @@ namespace {
 using LibDecFn = void (*)(const detail::LibDecArgs);
 // Knobs::lib_dec_wg = 64 (measurement build): 64-lane workgroups, 1 KiB tiles.
 uint32_t lib_dec_lanes() { return kMeasureBuild && knobs().lib_dec_wg == 64 ? 64u : (uint32_t)kThreads; }
+LibbDec libb_dec(int w, int k) {
+  const Knobs& kn = knobs();
+  const int la = kMeasureBuild ? kn.lib_dec_la : kLibbDecLA;
+  const int tw = kMeasureBuild ? kn.lib_dec_wg : kLibbDecTW;
+  switch (w) {
+    case 3: return libb_dec_pick<3>(k, la, tw);
+    case 5: return libb_dec_pick<5>(k, la, tw);
+    case 7: return libb_dec_pick<7>(k, la, tw);
+    case 11: return libb_dec_pick<11>(k, la, tw);
+    case 13: return libb_dec_pick<13>(k, la, tw);
+    default: return {nullptr, 0};
+  }
+}
 template <int W>
 LibDecFn lib_dec_kernel_w() {
 #ifdef LEOEC_MEASURE
@@ -315,7 +345,15 @@ bool lib_dec_supported(int w) {
 
 int launch(const LibDecApply& p, hipStream_t s) {
   const int w = p.w;
-  const LibDecFn fn = lib_dec_kernel(w);
+  LibDecFn fn = lib_dec_kernel(w);
+  uint32_t lanes = lib_dec_lanes();
+  if (knobs().lib_buf) {
+    const LibbDec b = libb_dec(w, p.k);
+    if (b.fn) {
+      fn = b.fn;
+      lanes = b.lanes;
+    }
+  }
   const int nout = (int)p.out.size();
   if (!fn || p.k <= 0 || p.k > w || (int)p.data.size() != p.k || p.cod.size() != 2 || nout < 1 ||
       nout > 2 || p.mbits.size() != (size_t)nout * 2 * w)
@@ -326,7 +364,6 @@ int launch(const LibDecApply& p, hipStream_t s) {
     for (const Shard& sh : *v)
       if (sh.base && (((uintptr_t)sh.base & 15u) || (sh.stride & 15u))) return LEOEC_E_ARG;
   const uint32_t ps = (uint32_t)(p.block_size / (uint64_t)w);
-  const uint32_t lanes = lib_dec_lanes();
   const uint32_t tb = lanes * 16u;
   const uint32_t tiles = (ps + tb - 1) / tb;
   const uint64_t max_obj = (uint64_t)0x7FFFFFFF / tiles;
@@ -367,9 +404,13 @@ int launch(const BitApply& p, hipStream_t s) {
   if (p.block_size == 0 || p.nobj == 0) return LEOEC_OK;
   if (p.block_size % ((uint64_t)16 * w) || p.block_size >= (1ull << 32)) return LEOEC_E_BAD_SIZE;
   if (!shards_ok(p.in) || !shards_ok(p.out)) return LEOEC_E_ARG;
-  if (knobs().lib_form != 0)
-    if (const LibFn lf = lib_kernel(w))
-      if (is_liberation_encode(p)) return launch_lib(p, lf, s);
+  if (knobs().lib_form != 0 && is_liberation_encode(p)) {
+    if (knobs().lib_buf) {
+      const LibbEnc b = libb_enc(w, p.KB);
+      if (b.fn) return launch_lib(p, b.fn, b.lanes, s);
+    }
+    if (const LibFn lf = lib_kernel(w)) return launch_lib(p, lf, lib_lanes(), s);
+  }
   const uint32_t ps = (uint32_t)(p.block_size / (uint64_t)w);
   const uint32_t tiles = (ps + kTileBytes - 1) / kTileBytes;
   const uint64_t max_obj = (uint64_t)0x7FFFFFFF / tiles;

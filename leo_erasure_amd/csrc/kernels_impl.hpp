@@ -822,6 +822,224 @@ lib_dec_apply(const LibDecArgs a) {
 }
 
 // ===========================================================================
+// Liberation encode and decode with branch-free loads (round 5).
+//
+// lib_apply / lib_dec_apply above pick per load between a plain load (tile
+// inside every shard) and load_guarded (a per-lane branch around the load).
+// The uniform `full` test sits inside the unrolled packet loop, so every
+// load sits between branches, and the compiler's wait-count pass then waits
+// for ALL outstanding loads at each one: the shipped lib_apply<7> has 98
+// loads and 79 `s_waitcnt vmcnt(0)` and no partial wait, so its "packets of
+// look-ahead" never overlap (a wave has one 1 KiB load in flight at a time).
+// Here the loads are raw buffer loads over one resource per block whose
+// records end at the block's valid length rounded up to 16 (past it a load
+// returns zeros without a memory access): no branch around any load, the
+// look-ahead is real, and the wave-uniform `full` decision is taken once per
+// tile, outside the loop (two copies of the body).  A tile that crosses a
+// valid length clears the straddling chunk's tail where the packet is
+// consumed (not where it is loaded, so its loads still overlap).  Absent
+// shards (blocks past k, erased data blocks, coding blocks not in the
+// survivor set) have base nullptr and valid 0: their loads return zeros.
+__device__ __forceinline__ u32x4 libb_load(__amdgpu_buffer_rsrc_t rs, uint32_t vo) {
+  return __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 2);  // nt
+}
+// An empty asm that "redefines" v: the XOR into v is done here, in ring
+// order.  Without it the XORs of the straight-line body are reassociated into
+// one tree at the end, so every loaded packet stays live (49 x 4 VGPRs at
+// w = 7: the body spills).
+__device__ __forceinline__ void libb_pin(u32x4& v) { asm volatile("" : "+v"(v)); }
+// Bytes at or past `valid` of the 16-byte chunk at `pos` cleared.
+__device__ __forceinline__ u32x4 libb_clip(u32x4 v, uint32_t valid, uint32_t pos) {
+  const uint32_t n = valid > pos ? (valid - pos < 16u ? valid - pos : 16u) : 0u;
+  return keep_first(v, n);
+}
+
+template <int W, int K, int LA, bool FULL>
+__device__ __forceinline__ void libb_enc_tile(const LibArgs& a, uint64_t o64, uint32_t off,
+                                              bool live) {
+  constexpr int RS = LA + 1;  // ring of packet registers: LA loads in flight
+  uint32_t vo[W];
+#pragma unroll
+  for (int x = 0; x < W; ++x) vo[x] = off + (uint32_t)x * a.ps;
+  // block j's resource, built where it is used (SGPR arithmetic; an array
+  // of resources is not promoted to registers at w >= 11)
+  auto rs = [&](int j) {
+    return shard_rsrc(a.in[j].base, a.in[j].stride, a.in[j].valid, o64, 16u);
+  };
+  u32x4 P[W], Q[W], ring[RS];
+#pragma unroll
+  for (int x = 0; x < W; ++x) P[x] = Q[x] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int q = 0; q < LA && q < K * W; ++q) ring[q] = libb_load(rs(q / W), vo[q % W]);
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const int y = (j * ((W - 1) / 2)) % W;  // Q row of block j's extra one
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const int p = j * W + x, q = p + LA;  // packet applied / packet loaded
+      if (q < K * W) ring[q % RS] = libb_load(rs(q / W), vo[q % W]);
+      u32x4 v = ring[p % RS];
+      if (!FULL) v = libb_clip(v, a.in[j].valid, vo[x]);
+      P[x] ^= v;
+      Q[(x - j + W) % W] ^= v;
+      libb_pin(P[x]);
+      libb_pin(Q[(x - j + W) % W]);
+      if (j > 0 && x == (y + j - 1) % W) {
+        Q[y] ^= v;
+        libb_pin(Q[y]);
+      }
+      // and the loads where the ring puts them (not hoisted further)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (!live) return;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    uint8_t* b = const_cast<uint8_t*>(a.out[r].base) + o64 * a.out[r].stride;
+    const uint32_t v = a.out[r].valid;
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const u32x4 acc = r == 0 ? P[x] : Q[x];
+      if (FULL) st16<true>(b + vo[x], acc);
+      else store_guarded(b, vo[x], v, acc);
+    }
+  }
+}
+
+template <int W, int K, int LA, int TW>
+__global__ void __launch_bounds__(TW) __attribute__((amdgpu_waves_per_eu(lib_waves(W), 8)))
+libb_apply(const LibArgs a) {
+  constexpr uint32_t kTileBytes = TW * 16u;
+  const uint32_t bid = a.xmap ? xcd_obj_map(blockIdx.x, gridDim.x, a.tiles) : blockIdx.x;
+  const uint32_t obj = bid / a.tiles;
+  const uint32_t tile = bid - obj * a.tiles;
+  const uint32_t t0 = tile * kTileBytes;
+  const uint32_t off = t0 + threadIdx.x * 16u;
+  // wave-uniform, as lib_apply's
+  const bool full = t0 + kTileBytes <= a.ps &&
+                    (uint64_t)(W - 1) * a.ps + t0 + kTileBytes <= (uint64_t)a.vmin;
+  // lanes past the packet (last tile) load and compute but do not store
+  if (full) libb_enc_tile<W, K, LA, true>(a, obj, off, true);
+  else libb_enc_tile<W, K, LA, false>(a, obj, off, off < a.ps);
+}
+
+template <int W, int K, int LA, bool FULL>
+__device__ __forceinline__ void libb_dec_tile(const LibDecArgs& a, uint64_t o64, uint32_t off,
+                                              bool live) {
+  constexpr int RS = LA + 1, NB = K + 2, NP = NB * W;
+  uint32_t vo[W];
+#pragma unroll
+  for (int x = 0; x < W; ++x) vo[x] = off + (uint32_t)x * a.ps;
+  // one packet stream: P (W packets), Q (W), then data blocks 0..k-1, as
+  // lib_dec_apply; absent shards read as zeros through an empty resource
+  auto shard_of = [&](int blk) -> const DevShard& {  // blk: 0 P, 1 Q, 2 + j data j
+    return blk < 2 ? a.cod[blk] : a.data[blk - 2];
+  };
+  auto rs = [&](int b) {
+    const DevShard& sh = shard_of(b);
+    return shard_rsrc(sh.base, sh.stride, sh.valid, o64, 16u);
+  };
+  u32x4 S[2 * W];  // P syndromes, then Q syndromes
+#pragma unroll
+  for (int s = 0; s < 2 * W; ++s) S[s] = u32x4{0u, 0u, 0u, 0u};
+  u32x4 ring[RS];
+#pragma unroll
+  for (int q = 0; q < LA; ++q) ring[q] = libb_load(rs(q / W), vo[q % W]);
+#pragma unroll
+  for (int blk = 0; blk < NB; ++blk) {
+    const int j = blk - 2;
+    const int y = j > 0 ? (j * ((W - 1) / 2)) % W : 0;
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      const int p = blk * W + x, q = p + LA;
+      if (q < NP) ring[q % RS] = libb_load(rs(q / W), vo[q % W]);
+      u32x4 v = ring[p % RS];
+      if (!FULL) v = libb_clip(v, shard_of(blk).valid, vo[x]);
+      if (blk < 2) {
+        S[blk * W + x] ^= v;
+        libb_pin(S[blk * W + x]);
+      } else {
+        S[x] ^= v;
+        S[W + (x - j + W) % W] ^= v;
+        libb_pin(S[x]);
+        libb_pin(S[W + (x - j + W) % W]);
+        if (j > 0 && x == (y + j - 1) % W) {
+          S[W + y] ^= v;
+          libb_pin(S[W + y]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // as libb_enc_tile
+    }
+  }
+  if (!live) return;
+  // (unrolled over the <= 2 wanted blocks: as a run-time loop, the edge
+  // path's byte-store addresses of both were hoisted out of it and spilled)
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    if (b >= a.nout) break;
+    u32x4 acc[W];
+#pragma unroll
+    for (int x = 0; x < W; ++x) acc[x] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int s = 0; s < 2 * W; ++s) {
+      const uint32_t bits = a.mbits[b][s];  // wave-uniform
+      if (bits != 0u) {
+#pragma unroll
+        for (int x = 0; x < W; ++x) {
+          const uint32_t m = (uint32_t)((int32_t)(bits << x) >> 31);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[x][e] ^= S[s][e] & m;
+        }
+      }
+    }
+    uint8_t* ob = const_cast<uint8_t*>(a.out[b].base) + o64 * a.out[b].stride;
+    const uint32_t v = a.out[b].valid;
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+      if (FULL) st16<true>(ob + vo[x], acc[x]);
+      else store_guarded(ob, vo[x], v, acc[x]);
+    }
+  }
+}
+
+template <int W, int K, int LA, int TW>
+__global__ void __launch_bounds__(TW) __attribute__((amdgpu_waves_per_eu(lib_dec_waves(W), 8)))
+libb_dec_apply(const LibDecArgs a) {
+  constexpr uint32_t kTileBytes = TW * 16u;
+  const uint32_t bid = a.xmap ? xcd_obj_map(blockIdx.x, gridDim.x, a.tiles) : blockIdx.x;
+  const uint32_t obj = bid / a.tiles;
+  const uint32_t tile = bid - obj * a.tiles;
+  const uint32_t t0 = tile * kTileBytes;
+  const uint32_t off = t0 + threadIdx.x * 16u;
+  const bool full = t0 + kTileBytes <= a.ps &&
+                    (uint64_t)(W - 1) * a.ps + t0 + kTileBytes <= (uint64_t)a.vmin;
+  if (full) libb_dec_tile<W, K, LA, true>(a, obj, off, true);
+  else libb_dec_tile<W, K, LA, false>(a, obj, off, off < a.ps);
+}
+
+// Launch tables of libb_apply / libb_dec_apply, one translation unit per w
+// (lib_inst.hip, every k = 1..w compiled in): the instance for (k, look-ahead
+// la, tw lanes), or the shipped (la, tw) when that form is not built
+// (measurement forms exist for the A/B configs only); fn nullptr for a w
+// without instances.
+using LibbEncFn = void (*)(const LibArgs);
+using LibbDecFn = void (*)(const LibDecArgs);
+struct LibbEnc {
+  LibbEncFn fn;
+  uint32_t lanes;
+};
+struct LibbDec {
+  LibbDecFn fn;
+  uint32_t lanes;
+};
+constexpr int kLibbEncLA = 2, kLibbEncTW = 64;    // shipped encode form
+constexpr int kLibbDecLA = 2, kLibbDecTW = 256;   // shipped decode form
+template <int W>
+LibbEnc libb_enc_pick(int k, int la, int tw);
+template <int W>
+LibbDec libb_dec_pick(int k, int la, int tw);
+
+// ===========================================================================
 // GF(2^w) on packet-bitsliced blocks (cauchyrs).  Each lane owns LW dwords of
 // every packet.  Per input block: y = its w packets; for t = 0..w-1, every
 // output block whose coefficient has bit t set gets y xor-ed in, then

@@ -67,6 +67,9 @@ struct Knobs {
   int lib_wg = 64;           // LEOEC_LIB_WG=256: lib_apply with 256-lane workgroups (4 KiB tiles)
   int lib_dec_wg = 256;      // LEOEC_LIB_DEC_WG=64: lib_dec_apply with 64-lane workgroups
   int lib_xmap = 2;          // LEOEC_LIB_XMAP=0: liberation kernels without xcd_obj_map
+  int lib_buf = 0;           // LEOEC_LIB_BUF=1: liberation encode / decode with branch-free raw
+                             //   buffer loads (libb_apply / libb_dec_apply, kernels_impl.hpp)
+  int lib_dec_la = 2;        // LEOEC_LIB_DEC_LA: libb_dec_apply packet look-ahead
   // gfbit_inst.hip
   int gfbit_xmap = -1;       // LEOEC_GFBIT_XMAP: 0 off, 1 object-contiguous, unset auto
   int gfbit_lw = 2;          // LEOEC_GFBIT_LW: lane width (dwords per packet), w = 8

@@ -14,9 +14,13 @@
 // host-memory call on the calling scheduler thread's current HIP device.  A
 // VM that should drive several GPUs sets LEOEC_HOST_DEVICES before starting
 // ("all", or a comma list of device ordinals): load passes the set to
-// leoec_host_spread, and calls then go to the least-loaded device of the set.
-// A malformed value fails the load; a set the runtime cannot serve (no GPU)
-// is left to the data calls, which report LEOEC_E_NO_DEVICE as usual.
+// leoec_host_spread (which warms every device of the set before returning),
+// and calls then go to the least-loaded device of the set.  A malformed
+// value fails the load, and so does a well-formed set naming a device the
+// process cannot use (say "0,1,7" on a 2-GPU node: leoec_host_spread refuses
+// it and would leave every call on the scheduler thread's current device);
+// the message goes to stderr.  Without any gfx950 device the value is left
+// to the data calls, which report LEOEC_E_NO_DEVICE as usual.
 //
 // -DLEOEC_NIF_REF_ERRORS reproduces the reference's error terms exactly: its
 // coder exceptions are rethrown by value as std::exception
@@ -31,6 +35,7 @@
 #ifdef HAVE_ERL_NIF
 #include <erl_nif.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -250,9 +255,19 @@ bool parse_host_devices(const char* e, std::vector<int>* devs) {
 }
 
 int nif_load(ErlNifEnv*, void**, ERL_NIF_TERM) {
+  const char* spec = std::getenv("LEOEC_HOST_DEVICES");
   std::vector<int> devs;
-  if (!parse_host_devices(std::getenv("LEOEC_HOST_DEVICES"), &devs)) return 1;
-  if (!devs.empty()) (void)leoec_host_spread(devs.data(), (int)devs.size());
+  if (!parse_host_devices(spec, &devs)) {
+    std::fprintf(stderr, "leo_erasure: malformed LEOEC_HOST_DEVICES=\"%s\"\n", spec);
+    return 1;
+  }
+  if (devs.empty()) return 0;
+  const int rc = leoec_host_spread(devs.data(), (int)devs.size());
+  if (rc < 0 && leoec_host_lanes(nullptr, 0) > 0) {  // devices exist, the set is not theirs
+    std::fprintf(stderr, "leo_erasure: LEOEC_HOST_DEVICES=\"%s\": %s\n", spec,
+                 leoec_strerror(rc));
+    return 2;
+  }
   return 0;
 }
 

@@ -784,10 +784,74 @@ __attribute__((target("avx2"))) static void apply_avx2(int nin, int nout, const 
 #endif
 
 #if defined(__x86_64__)
+/* ISA-L's gf_Nvect_dot_prod_avx512_gfni shape for N = nout <= 4 output rows:
+ * the row count compiled in (NOUT is a literal at every call site of this
+ * always-inline body), so the accumulators live in zmm registers, not in a
+ * run-time-indexed array on the stack; two 64-byte vectors per iteration (two
+ * independent XOR chains per row); each coefficient's affine matrix is a
+ * broadcast memory operand of vgf2p8affineqb.  Returns the bytes done (a
+ * multiple of 128; the caller finishes the rest). */
+__attribute__((target("avx512f,avx512bw,gfni"), always_inline)) static inline uint64_t
+gfni_rows(int nin, const int NOUT, const uint64_t *mats, const uint8_t *const *in,
+          uint8_t *const *out, uint64_t len) {
+  uint64_t i = 0;
+  for (; i + 128 <= len; i += 128) {
+    __m512i a0 = _mm512_setzero_si512(), a1 = a0, a2 = a0, a3 = a0;
+    __m512i b0 = a0, b1 = a0, b2 = a0, b3 = a0;
+    for (int j = 0; j < nin; j++) {
+      const __m512i x = _mm512_loadu_si512((const void *)(in[j] + i));
+      const __m512i y = _mm512_loadu_si512((const void *)(in[j] + i + 64));
+      const uint64_t *mj = mats + j;
+#define GF_ROW(o, A, B)                                                          \
+      if (NOUT > o) {                                                            \
+        const __m512i M = _mm512_set1_epi64((long long)mj[(size_t)(o) * nin]);   \
+        A = _mm512_xor_si512(A, _mm512_gf2p8affine_epi64_epi8(x, M, 0));         \
+        B = _mm512_xor_si512(B, _mm512_gf2p8affine_epi64_epi8(y, M, 0));         \
+      }
+      GF_ROW(0, a0, b0)
+      GF_ROW(1, a1, b1)
+      GF_ROW(2, a2, b2)
+      GF_ROW(3, a3, b3)
+#undef GF_ROW
+    }
+    _mm512_storeu_si512((void *)(out[0] + i), a0);
+    _mm512_storeu_si512((void *)(out[0] + i + 64), b0);
+    if (NOUT > 1) {
+      _mm512_storeu_si512((void *)(out[1] + i), a1);
+      _mm512_storeu_si512((void *)(out[1] + i + 64), b1);
+    }
+    if (NOUT > 2) {
+      _mm512_storeu_si512((void *)(out[2] + i), a2);
+      _mm512_storeu_si512((void *)(out[2] + i + 64), b2);
+    }
+    if (NOUT > 3) {
+      _mm512_storeu_si512((void *)(out[3] + i), a3);
+      _mm512_storeu_si512((void *)(out[3] + i + 64), b3);
+    }
+  }
+  return i;
+}
+
 __attribute__((target("avx512f,avx512bw,gfni"))) static void apply_gfni(
     int nin, int nout, const uint64_t *mats, const uint8_t *tbl, const uint8_t *const *in,
     uint8_t *const *out, uint64_t len) {
   uint64_t i = 0;
+  /* the rows in groups of at most 4, each group one specialised pass (ISA-L
+   * runs m > 6 rows as several passes the same way) */
+  if (nout <= 16) {
+    uint64_t done = len;
+    for (int o0 = 0; o0 < nout; o0 += 4) {
+      const int n = nout - o0 < 4 ? nout - o0 : 4;
+      const uint64_t *mo = mats + (size_t)o0 * nin;
+      uint8_t *const *oo = out + o0;
+      const uint64_t d = n == 4   ? gfni_rows(nin, 4, mo, in, oo, len)
+                         : n == 3 ? gfni_rows(nin, 3, mo, in, oo, len)
+                         : n == 2 ? gfni_rows(nin, 2, mo, in, oo, len)
+                                  : gfni_rows(nin, 1, mo, in, oo, len);
+      done = d;
+    }
+    i = nout > 0 ? done : len;
+  }
   for (; i + 64 <= len; i += 64) {
     __m512i acc[16];
     for (int o = 0; o < nout; o++) acc[o] = _mm512_setzero_si512();

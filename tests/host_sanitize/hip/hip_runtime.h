@@ -175,6 +175,15 @@ inline Pinned& pinned() {
   return *p;
 }
 
+// Fault injection: the n-th hipEventCreateWithFlags of the calling thread
+// from now on fails (0: none).  host_stress uses it to fail the second
+// column chunk of a per-thread zero-copy call (engine.cpp zc_chunked).
+inline int& fail_event_create_in() {
+  static thread_local int n = 0;
+  return n;
+}
+inline void fail_nth_event_create(int n) { fail_event_create_in() = n; }
+
 inline std::atomic<long>& live_allocs() {
   static std::atomic<long> n{0};
   return n;
@@ -309,6 +318,11 @@ inline hipError_t hipHostUnregister(void* p) {
 }
 
 inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) {
+  int& n = fakehip::fail_event_create_in();
+  if (n > 0 && --n == 0) {
+    *e = nullptr;
+    return hipErrorOutOfMemory;
+  }
   *e = new fakehip::Event;
   return hipSuccess;
 }

@@ -171,3 +171,31 @@ def test_warmup_passes_precede_the_timed_ones(oracle):
     oracle.bench_rs8_pinned(10, 4, objs, size, [0, 1, 2, 3], 2, None, 0.02, 0.06,
                             warm_s=0.0, warmup=warm0)
     assert warm0 == []
+
+
+def _leg(value, equal=True, structure="x"):
+    return {"value": value, "parity_vs_gpu": {"objects": 4, "equal": equal},
+            "structure": structure, "cores": 15, "workers": 15, "share_cpus": 16,
+            "kind": "port", "pinning": {"cpus": [0]}}
+
+
+@pytest.mark.parametrize("port,ref,top", [
+    (108.6, 113.5, "reference_structure"),  # the round-4 driver box: Jerasure's structure faster
+    (117.7, 92.0, "isa_l_port"),
+    (100.0, 130.0, "isa_l_port"),            # a faster leg whose parity differs never heads
+])
+def test_headline_is_the_faster_parity_equal_leg(port, ref, top):
+    """cpu_baseline.value is the strongest CPU figure of the line (round-4
+    verdict item 3): the faster of the two SIMD legs whose output equals the
+    GPU's, the other kept under its name; the full-share estimate scales it
+    by share / workers (round-4 advisor)."""
+    ref_ok = not (port == 100.0)
+    rec = bench.headline_cpu(_leg(port, structure="ISA-L"), _leg(ref, ref_ok, "Jerasure"))
+    assert rec["headline_leg"] == top
+    want = {"isa_l_port": port, "reference_structure": ref}
+    assert rec["value"] == want[top]
+    other = [x for x in bench.CPU_LEGS if x != top][0]
+    assert rec[other]["value"] == want[other]
+    assert rec["structure"] == ("ISA-L" if top == "isa_l_port" else "Jerasure")
+    assert rec["cores"] == 15 and rec["pinning"] == {"cpus": [0]}
+    assert rec["full_share_estimate_GiBps"] == pytest.approx(want[top] * 16 / 15, rel=1e-3)

@@ -58,6 +58,25 @@ class CpuBackend:
     def event(self):
         return CpuEvent()
 
+    def host_path(self, objs, parity, size, bs, callers=32, seconds=1.0):
+        """bench.GpuBackend.host_path's record over the oracle's one-object
+        calls (the host-memory API's outputs: tail data block + parity)."""
+        from oracle import oracle as O
+        n = min(callers, objs.shape[0], 2)
+        t0 = time.perf_counter()
+        enc_ok = dec_ok = True
+        for t in range(n):
+            data = objs[t, :size].numpy().tobytes()
+            blocks = O.encode("vandrs", bench.K, bench.M, bench.W, data)
+            enc_ok &= b"".join(blocks[bench.K:]) == parity[t].numpy().tobytes()
+            dec_ok &= b"".join(blocks[:bench.K])[:size] == data
+        dt = max(time.perf_counter() - t0, 1e-9)
+        rate = n * size / dt / 2**30
+        return {"encode_GiBps": round(rate, 4), "decode_GiBps": round(rate, 4), "callers": n,
+                "seconds_per_op": seconds, "calls": [n, n],
+                "parity_vs_gpu": {"objects": n, "encode_equal": enc_ok, "decode_equal": dec_ok},
+                "what": "cpu stub"}
+
 
 class NoopDecode(CpuBackend):
     def decode(self, objs, size, parity, erased):
@@ -69,7 +88,22 @@ class ZeroEncode(CpuBackend):
         parity.zero_()
 
 
-BACKENDS = {"cpu": CpuBackend, "noop_decode": NoopDecode, "zero_encode": ZeroEncode}
+class BadHost(CpuBackend):
+    """Rank 1's host-memory leg reports parity that differs from the GPU's."""
+
+    def __init__(self, local_rank, world, oversubscribe=False):
+        super().__init__(local_rank, world, oversubscribe)
+        self.rank = local_rank
+
+    def host_path(self, *a, **kw):
+        rec = super().host_path(*a, **kw)
+        if self.rank == 1:
+            rec["parity_vs_gpu"]["encode_equal"] = False
+        return rec
+
+
+BACKENDS = {"cpu": CpuBackend, "noop_decode": NoopDecode, "zero_encode": ZeroEncode,
+            "bad_host": BadHost}
 
 
 def _free_port():
@@ -137,6 +171,29 @@ def test_two_ranks_weak_scaling_through_bench_main():
             assert r[fkey] == pytest.approx(5 * per_obj / (r[key] * 1e-3) / 1e9 / 8000.0,
                                             rel=1e-2, abs=6e-5)
     assert rec["cpu_parity_checked"] is False
+    # the host-memory leg: every rank its own, the node's rate their sum
+    hp = rec["host_path"]
+    assert len(hp["per_rank"]) == 2
+    for op in ("encode_GiBps", "decode_GiBps"):
+        assert hp[op] == pytest.approx(sum(h[op] for h in hp["per_rank"]), abs=0.006)
+    assert all(h["parity_vs_gpu"]["encode_equal"] and h["parity_vs_gpu"]["decode_equal"]
+               for h in hp["per_rank"])
+    assert hp["callers"] == sum(h["callers"] for h in hp["per_rank"])
+
+
+def test_host_leg_parity_failure_fails_the_line():
+    """A host-path leg whose outputs differ from the GPU's fails `verified`."""
+    res = _run_ranks(2, ["--gpus", "2", "--objects", "3"] + SMALL, backend="bad_host")
+    (r0, rc0, out0), (r1, rc1, out1) = res
+    rec = json.loads(out0)
+    assert rec["verified"] is False and rc0 == 1
+    assert rec["host_path"]["per_rank"][1]["parity_vs_gpu"]["encode_equal"] is False
+
+
+def test_host_leg_can_be_skipped():
+    res = _run_ranks(2, ["--gpus", "2", "--objects", "3", "--no-host"] + SMALL)
+    rec = json.loads(res[0][2])
+    assert "host_path" not in rec and rec["verified"] is True
 
 
 def test_two_ranks_partitioned_batch():
@@ -171,10 +228,15 @@ def test_single_rank_cpu_leg_checks_parity(monkeypatch):
     assert cb["workers"] == cb["cores"] and cb["cores"] <= max(1, cb["share_cpus"] - 1)
     assert len(cb["throttled_s_per_pass"]) == len(cb["passes_GiBps"])
     assert len(cb["warmup_passes_GiBps"]) >= 1
-    # the reference's own CPU structure, same sample, same parity check
-    rs = cb["reference_structure"]
-    assert rs["parity_vs_gpu"] == {"objects": 3, "equal": True}
-    assert rs["value"] > 0 and "Jerasure" in rs["structure"] and rs["cores"] == cb["cores"]
+    # both SIMD legs (the ISA-L-technique port and the reference's own CPU
+    # structure), same sample, same parity check; the faster one on top
+    top = cb["headline_leg"]
+    assert top in bench.CPU_LEGS
+    other = cb[[x for x in bench.CPU_LEGS if x != top][0]]
+    assert other["parity_vs_gpu"] == {"objects": 3, "equal": True}
+    assert other["value"] > 0 and other["cores"] == cb["cores"] and cb["value"] >= other["value"]
+    rs = cb if top == "reference_structure" else other
+    assert "Jerasure" in rs["structure"]
     sc = cb["scalar"]
     assert sc["parity_vs_gpu"] == {"objects": 3, "equal": True} and sc["simd"] == "scalar"
     assert rec["cpu_parity_checked"] is True
@@ -202,20 +264,21 @@ def test_single_rank_failed_cpu_leg_is_recorded(monkeypatch):
 class WithCeiling(CpuBackend):
     calls = []
 
-    def pattern_ceiling(self, objs, size, parity, enc_bytes):
-        WithCeiling.calls.append((objs.shape[0], size, enc_bytes))
+    def pattern_ceiling_child(self, n, size, seed):
+        WithCeiling.calls.append((n, size, seed))
         return {"achieved": 1.0, "shipped_over_ceiling": 0.5}
 
 
 class BrokenCeiling(CpuBackend):
-    def pattern_ceiling(self, objs, size, parity, enc_bytes):
+    def pattern_ceiling_child(self, n, size, seed):
         raise RuntimeError("no measurement build")
 
 
 def test_single_rank_pattern_ceiling_leg(monkeypatch):
     """The live pattern-ceiling leg runs once at N = 1 after the timed region
-    (on the rank's batch and its encode bytes) and lands in `roofline`; a
-    failing leg is recorded and never fails the measurement."""
+    (in a child process that regenerates the rank's seeded batch: the bench
+    process loads one HIP library) and lands in `roofline`; a failing leg is
+    recorded and never fails the measurement."""
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     argv = ["--objects", "3", "--no-cpu"] + SMALL
     out = io.StringIO()
@@ -224,7 +287,7 @@ def test_single_rank_pattern_ceiling_leg(monkeypatch):
     rec = json.loads(out.getvalue())
     assert rc == 0 and rec["verified"] is True
     assert rec["roofline"]["pattern_ceiling"] == {"achieved": 1.0, "shipped_over_ceiling": 0.5}
-    assert WithCeiling.calls == [(3, 65536, rec["roofline"]["alg_bytes_per_launch"])]
+    assert WithCeiling.calls == [(3, 65536, 0x1E0E)]  # the batch's own seed
     out = io.StringIO()
     with contextlib.redirect_stdout(out):
         rc = bench.main(argv, backend=BrokenCeiling)

@@ -3,6 +3,7 @@ oracle, on the reference's own test configurations (test/leo_erasure_tests.erl)
 plus the BASELINE configs.  Bit-exact everywhere (integer / byte arithmetic).
 """
 import itertools
+import json
 import os
 import random
 import subprocess
@@ -535,3 +536,51 @@ def test_host_spread_opt_in(gpu, le, oracle):
     ids = list(range(4, 14))
     st, out = le.nif_decode("vandrs", (10, 4, 8), [ref[i] for i in ids], ids, len(data))
     assert st == "ok" and out == data
+
+
+_WARM_CHILD = r"""
+import json, sys, time
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import torch
+import leo_erasure_amd as le
+from oracle import oracle as O
+torch.cuda.set_device(0)
+before = le._lib.measure_warm_state(0)
+t0 = time.perf_counter()
+n = le._lib.host_spread([0])
+t_spread = time.perf_counter() - t0
+after = le._lib.measure_warm_state(0)
+data = bytes(range(256)) * 4096 + b"tail"
+t0 = time.perf_counter()
+st, blocks = le.nif_encode("vandrs", (10, 4, 8), data, len(data))
+t_first = time.perf_counter() - t0
+final = le._lib.measure_warm_state(0)
+le._lib.host_spread([])
+print(json.dumps({"n": n, "before": before, "after": after, "final": final,
+                  "t_spread": t_spread, "t_first": t_first, "ok": st == "ok",
+                  "parity": blocks == O.encode("vandrs", 10, 4, 8, data)}))
+"""
+
+
+def test_host_spread_warms_its_devices(gpu):
+    """leoec_host_spread warms every device of its set before returning (as
+    gf_init warms the caller's device): in a fresh process that never called
+    gf_init, host_spread([0]) builds device 0's batching queue and pools, and
+    the first host call afterwards builds no queue and pays no start-up.
+    Child process on the measurement build (its warm-state counters)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.exists(os.path.join(root, "leo_erasure_amd", "libleoec_measure.so")):
+        pytest.skip("measurement build absent (make -C leo_erasure_amd/csrc measure)")
+    env = dict(os.environ, LEOEC_LIBRARY="measure")
+    r = subprocess.run([sys.executable, "-c", _WARM_CHILD, root, os.path.join(root, "tests")],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["n"] == 1
+    assert not out["before"]["queue"] and out["before"]["queues_built"] == 0
+    assert out["after"]["queue"] and out["after"]["queues_built"] == 1
+    assert out["after"]["pool_streams"] >= 1 and out["after"]["pool_mapped"] >= 1
+    assert out["final"]["queues_built"] == 1, "the first call after host_spread built a queue"
+    assert out["ok"] and out["parity"]
+    # a cold first call pays ~150-250 ms of runtime and queue set-up
+    assert out["t_first"] < 0.05, out

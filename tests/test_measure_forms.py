@@ -85,6 +85,27 @@ def test_liberation_encode_forms(gpu, le, oracle, form, measure):
         measure.setenv("LEOEC_LIB_LA", "4")
     if form.endswith("decwg64"):
         measure.setenv("LEOEC_LIB_DEC_WG", "64")
+    _liberation_roundtrips(le, oracle)
+
+
+@pytest.mark.parametrize("env", [{}, {"LEOEC_LIB_LA": "4"}, {"LEOEC_LIB_LA": "8"},
+                                 {"LEOEC_LIB_WG": "256"}, {"LEOEC_LIB_WG": "256", "LEOEC_LIB_LA": "4"},
+                                 {"LEOEC_LIB_DEC_WG": "64"}, {"LEOEC_LIB_DEC_LA": "4"},
+                                 {"LEOEC_LIB_DEC_LA": "8", "LEOEC_LIB_DEC_WG": "64"}],
+                         ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()) or "shipped")
+def test_liberation_buffer_load_forms(gpu, le, oracle, env, measure):
+    """libb_apply / libb_dec_apply (LEOEC_LIB_BUF=1: branch-free raw buffer
+    loads, the block count compiled in, one instance per (w, k)): every w, k
+    from 1 to w, ragged sizes (tiles that cross a block's valid length clear
+    the straddling chunk's tail where it is consumed), the look-ahead and
+    lane-count forms built for the A/B configurations, against the oracle."""
+    measure.setenv("LEOEC_LIB_BUF", "1")
+    for k, v in env.items():
+        measure.setenv(k, v)
+    _liberation_roundtrips(le, oracle)
+
+
+def _liberation_roundtrips(le, oracle):
     for w in (3, 5, 7, 11, 13):
         for k in sorted({1, 2, (w + 1) // 2, w}):
             for size in (1, 4097, 150001):
@@ -109,24 +130,42 @@ def test_liberation_encode_forms(gpu, le, oracle, form, measure):
                 assert st == "ok" and rep == [blocks[1]], (k, w)
 
 
-def test_liberation_device_batch_forms(gpu, le, oracle, measure):
-    """Device-resident batch (ragged object size, 37 objects) through both
-    liberation encode forms: identical parity, equal to the oracle."""
-    k, m, w = 7, 2, 7
-    n, size = 37, 300007
+@pytest.mark.parametrize("k,w,size", [(7, 7, 300007), (4, 7, 1048576), (10, 11, 1048573)])
+def test_liberation_device_batch_forms(gpu, le, oracle, measure, k, w, size):
+    """Device-resident batch (37 objects, bytes past each object's size
+    random) through every liberation encode form — lib_apply, libb_apply
+    (LEOEC_LIB_BUF=1) and the generic masked kernel — and the two syndrome
+    decode forms: identical outputs, equal to the oracle."""
+    m = 2
+    n = 37
     bs, _ = le.layout("liberation", (k, m, w), size)
-    host, objs = _batch(gpu, n, size, size + 9 - (size + 9) % 16 + 16, 21)
+    stride = max(k * bs, size + 9 - (size + 9) % 16 + 16)
+    host, objs = _batch(gpu, n, size, stride, 21 + k)
     outs = []
-    for form in ("1", "0"):
+    for form, buf in (("1", "0"), ("1", "1"), ("0", "0")):
         measure.setenv("LEOEC_LIB_FORM", form)
+        measure.setenv("LEOEC_LIB_BUF", buf)
         parity = gpu.full((n, m * bs), 0x5A, dtype=gpu.uint8, device="cuda")
         le.device.encode("liberation", (k, m, w), objs, size, parity)
         gpu.cuda.synchronize()
         outs.append(parity.cpu().numpy())
-    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
     for o in range(0, n, 6):
         ref = oracle.encode("liberation", k, m, w, host[o, :size].tobytes())
         assert outs[0][o].tobytes() == b"".join(ref[k:]), f"object {o}"
+    # decode of two lost data blocks (syndromes through P and Q) in place
+    measure.setenv("LEOEC_LIB_FORM", "1")
+    parity = gpu.from_numpy(outs[0]).cuda()
+    lost = [0, k - 1]
+    for buf in ("0", "1"):
+        measure.setenv("LEOEC_LIB_BUF", buf)
+        dec = objs.clone()
+        for j in lost:
+            lo, hi = j * bs, min((j + 1) * bs, size)
+            dec[:, lo:hi] = 0xA5
+        le.device.decode("liberation", (k, m, w), dec, size, parity, lost)
+        gpu.cuda.synchronize()
+        assert gpu.equal(dec[:, :size], objs[:, :size]), f"decode LIB_BUF={buf}"
 
 
 @pytest.mark.parametrize("wg", ["64", "256"])

@@ -329,14 +329,7 @@ def test_gpu_engine_errors_through_shim(nif, gpu, le):
                         len(DATA))) == le.strerror(-13)
 
 
-@pytest.mark.parametrize("spec,rc", [(None, 0), ("", 0), ("all", 0), ("0", 0), ("0,1,7", 0),
-                                     ("0,x", 1), (",", 1), ("1,", 1), ("-1", 1), ("gpu0", 1)])
-def test_load_host_devices(nif, spec, rc):
-    """The shim's load callback (the reference registers none): the
-    LEOEC_HOST_DEVICES opt-in to spreading host calls over several GPUs is
-    parsed at load; a malformed value fails the load, a well-formed one that
-    the runtime cannot serve (no GPU here) is left to the data calls.  Run in
-    a child process: the test never writes its own environment."""
+def _load_with(nif, spec):
     import subprocess
     import sys
     code = ("import sys; sys.path[:0] = [%r, %r]\n"
@@ -349,4 +342,32 @@ def test_load_host_devices(nif, spec, rc):
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
                          timeout=120, env=env)
     assert out.returncode == 0, out.stderr[-2000:]
-    assert int(out.stdout.strip().splitlines()[-1]) == rc
+    return int(out.stdout.strip().splitlines()[-1]), out.stderr
+
+
+@pytest.mark.parametrize("spec,rc", [(None, 0), ("", 0), ("all", 0), ("0", 0), ("0,1,7", 0),
+                                     ("0,x", 1), (",", 1), ("1,", 1), ("-1", 1), ("gpu0", 1)])
+def test_load_host_devices(nif, spec, rc):
+    """The shim's load callback (the reference registers none): the
+    LEOEC_HOST_DEVICES opt-in to spreading host calls over several GPUs is
+    parsed at load; a malformed value fails the load, a well-formed one that
+    the runtime cannot serve (no GPU here) is left to the data calls.  Run in
+    a child process: the test never writes its own environment."""
+    if spec not in (None, "", "0,x", ",", "1,", "-1", "gpu0"):
+        import leo_erasure_amd as le
+        if le.lib.leoec_host_lanes(None, 0) > 0:
+            pytest.skip("a GPU is present: test_load_host_devices_on_gpu")
+    assert _load_with(nif, spec)[0] == rc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec,rc", [("all", 0), ("0", 0), ("0,63", 2), ("63", 2)])
+def test_load_host_devices_on_gpu(nif, spec, rc):
+    """With a GPU present, a well-formed LEOEC_HOST_DEVICES naming a device
+    the process cannot use fails the load (exit status 2, message on stderr)
+    instead of silently leaving every call on the scheduler thread's current
+    device (round-4 advisor)."""
+    got, err = _load_with(nif, spec)
+    assert got == rc, err[-2000:]
+    if rc:
+        assert "LEOEC_HOST_DEVICES" in err

@@ -18,8 +18,9 @@ def main():
     ap.add_argument("--w", type=int, default=8)
     ap.add_argument("--size", type=int, default=1 << 20)
     ap.add_argument("--objects", type=int, default=1024)
-    ap.add_argument("--op", choices=["encode", "decode"], default="encode")
-    ap.add_argument("--erased", default="0,1,2,3")
+    ap.add_argument("--op", choices=["encode", "decode", "repair"], default="encode")
+    ap.add_argument("--erased", default="0,1,2,3",
+                    help="decode: data blocks lost; repair: block ids rebuilt")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--knobs", default="",
                     help="K=V,K=V: measurement-build knobs (loads libleoec_measure.so)")
@@ -41,11 +42,24 @@ def main():
     par = torch.zeros((args.objects, stride), dtype=torch.uint8, device="cuda")
     er = [int(x) for x in args.erased.split(",")]
     le.device.encode(args.coding, p, objs, args.size, par)
+    if args.op == "repair":
+        # survivors: every block but the rebuilt ones, as [n][stride] row
+        # views (data blocks in the object rows, coding blocks in the parity
+        # rows); the rebuilt blocks go to one [n][r*bs] buffer (repair reads
+        # at the encode's rate with its outputs adjacent)
+        k, m = args.k, args.m
+        blocks = [objs[:, j * bs:] if j < k else par[:, (j - k) * bs:] for j in range(k + m)]
+        for i in er:
+            blocks[i] = None
+        out = torch.empty((args.objects, len(er) * bs), dtype=torch.uint8, device="cuda")
+        outs = [out[:, r * bs:] for r in range(len(er))]
     for _ in range(args.reps):
         if args.op == "encode":
             le.device.encode(args.coding, p, objs, args.size, par)
-        else:
+        elif args.op == "decode":
             le.device.decode(args.coding, p, objs, args.size, par, er)
+        else:
+            le.device.repair(args.coding, p, blocks, bs, er, outs, args.objects)
     torch.cuda.synchronize()
     print("one_op done", args.coding, p, args.op, "bs", bs)
 

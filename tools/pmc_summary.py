@@ -23,10 +23,14 @@ def summarise(d, frag):
         if per:
             out.update(per[max(per)])
     for f in glob.glob(os.path.join(d, "kt", "**", "*kernel_stats.csv"), recursive=True):
+        best = None  # the matching kernel launched most often (not a warm-up launch)
         for r in csv.DictReader(open(f)):
-            if frag in r["Name"]:
-                out["avg_ns"] = float(r["AverageNs"])
-                out["calls"] = int(r["Calls"])
+            if frag in r["Name"] and (best is None or int(r["Calls"]) > int(best["Calls"])):
+                best = r
+        if best:
+            out["avg_ns"] = float(best["AverageNs"])
+            out["calls"] = int(best["Calls"])
+            out["kernel"] = best["Name"]
     return out
 
 
