@@ -197,12 +197,19 @@ int bit_rows(const Code& c, const int* surv, const int* want, int nwant,
   return LEOEC_OK;
 }
 
-// Liberation decode / repair of erased data blocks as syndromes + a small
-// inverse (kernels_impl.hpp lib_dec_apply).  Applies when every wanted block
-// is an erased data block (not in the survivor set); LEOEC_E_UNSUPPORTED
-// sends the caller to the generic bitmatrix path (wanted coding blocks,
-// encode).  E = data ids missing from S, C = coding ids in S, |C| = |E|;
-// the map is rows(wanted) of (B_CE)^-1 applied to S_C = B_CS' D_S' ^ C.
+// Liberation decode / repair through syndromes + a small inverse
+// (kernels_impl.hpp lib_dec_apply).  E = data ids missing from S, C = coding
+// ids in S, |C| = |E|.  With absent shards read as zero, the kernel's
+// syndromes are S_r = B_rS' D_S' ^ [r in C] Code_r for r = P, Q, and since
+// Code_r = B_r D over every data block:
+//   r in C:      S_r = B_rE D_E,            so D_E = (B_CE)^-1 S_C;
+//   r not in C:  Code_r = S_r ^ B_rE D_E = S_r ^ B_rE (B_CE)^-1 S_C.
+// Every wanted block (an erased data block, or a coding block not in S: the
+// repair of {data, P} or {Q}, round 5) is thus one GF(2) map of the 2w
+// syndrome packets, sent as masks (mbits[b][s], bit 31 - x: syndrome packet s
+// feeds output packet x).  LEOEC_E_UNSUPPORTED sends the caller to the generic
+// bitmatrix path: the encode (all data present, P and Q wanted: lib_apply),
+// more than two wanted blocks, or a wanted block that is a survivor.
 int lib_dec_plan(const Code& c, const int* surv, const int* want, int nwant, Plan* p) {
   const int k = c.k, w = c.w;
   if (c.m != 2 || nwant < 1 || nwant > 2) return LEOEC_E_UNSUPPORTED;
@@ -216,31 +223,51 @@ int lib_dec_plan(const Code& c, const int* surv, const int* want, int nwant, Pla
     if (pos[j] < 0) E.push_back(j);
   for (int r = 0; r < 2; ++r)
     if (pos[k + r] >= 0) C.push_back(r);
-  if (E.empty() || E.size() != C.size()) return LEOEC_E_UNSUPPORTED;
-  std::vector<int> wi(nwant);  // wanted block -> index in E
-  for (int b = 0; b < nwant; ++b) {
-    const auto it = std::find(E.begin(), E.end(), want[b]);
-    if (it == E.end()) return LEOEC_E_UNSUPPORTED;
-    wi[b] = (int)(it - E.begin());
-  }
+  if (E.size() != C.size()) return LEOEC_E_UNSUPPORTED;
+  for (int b = 0; b < nwant; ++b)
+    if (want[b] < 0 || want[b] >= k + 2 || pos[want[b]] >= 0 ||
+        (want[b] >= k && !knobs().lib_dec_cod))
+      return LEOEC_E_UNSUPPORTED;
+  if (E.empty() && nwant == 2) return LEOEC_E_UNSUPPORTED;  // the encode: lib_apply
   const int e = (int)E.size(), n = e * w;
   BitMatrix A, inv;  // A = B_CE: rows of C's coding blocks, columns of E's data blocks
-  A.resize(n, n);
-  for (int ic = 0; ic < e; ++ic)
-    for (int r = 0; r < w; ++r)
-      for (int ie = 0; ie < e; ++ie)
-        for (int x = 0; x < w; ++x)
-          if (c.B.get(C[ic] * w + r, E[ie] * w + x)) A.set(ic * w + r, ie * w + x, true);
-  const int rc = bit_invert(A, &inv);
-  if (rc) return rc;
+  if (e > 0) {
+    A.resize(n, n);
+    for (int ic = 0; ic < e; ++ic)
+      for (int r = 0; r < w; ++r)
+        for (int ie = 0; ie < e; ++ie)
+          for (int x = 0; x < w; ++x)
+            if (c.B.get(C[ic] * w + r, E[ie] * w + x)) A.set(ic * w + r, ie * w + x, true);
+    const int rc = bit_invert(A, &inv);
+    if (rc) return rc;
+  }
   p->lib_pos = pos;
   p->mbits.assign((size_t)nwant * 2 * w, 0u);
-  for (int b = 0; b < nwant; ++b)
-    for (int x = 0; x < w; ++x)
+  for (int b = 0; b < nwant; ++b) {
+    uint32_t* mb = p->mbits.data() + (size_t)b * 2 * w;
+    const int id = want[b];
+    if (id < k) {  // an erased data block: its rows of (B_CE)^-1 over S_C
+      const int ie = (int)(std::find(E.begin(), E.end(), id) - E.begin());
+      for (int x = 0; x < w; ++x)
+        for (int ic = 0; ic < e; ++ic)
+          for (int r = 0; r < w; ++r)
+            if (inv.get(ie * w + x, ic * w + r)) mb[C[ic] * w + r] |= 1u << (31 - x);
+      continue;
+    }
+    // a coding block r not in S: S_r ^ B_rE (B_CE)^-1 S_C
+    const int rb = id - k;
+    for (int y = 0; y < w; ++y) {
+      mb[rb * w + y] |= 1u << (31 - y);
       for (int ic = 0; ic < e; ++ic)
-        for (int r = 0; r < w; ++r)
-          if (inv.get(wi[b] * w + x, ic * w + r))
-            p->mbits[(size_t)b * 2 * w + C[ic] * w + r] |= 1u << (31 - x);
+        for (int rr = 0; rr < w; ++rr) {
+          bool bit = false;  // (B_rE inv)[y][ic w + rr]
+          for (int ie = 0; ie < e; ++ie)
+            for (int x = 0; x < w; ++x)
+              bit ^= c.B.get(rb * w + y, E[ie] * w + x) && inv.get(ie * w + x, ic * w + rr);
+          if (bit) mb[C[ic] * w + rr] |= 1u << (31 - y);
+        }
+    }
+  }
   return LEOEC_OK;
 }
 
@@ -306,6 +333,7 @@ int make_plan(const Code& c, const int* surv, const int* want, int nwant,
   key.push_back((intptr_t)&c);
   key.push_back(knobs().bitmatrix);
   key.push_back(knobs().lib_form);
+  key.push_back(knobs().lib_dec_cod);
   key.push_back(nwant);
   key.insert(key.end(), surv, surv + c.k);
   key.insert(key.end(), want, want + nwant);
@@ -1503,7 +1531,8 @@ int op_repair_dev(int coding, int k, int m, int w, const uint8_t* const* blocks,
 // launch (1-2 ms each).  Here, on the caller's current device: this thread's
 // staging stream, one small pageable copy each way, and one small launch
 // into every kernel code object of the library (gf8 for K = 1..16, the
-// packet-bitsliced kernel for w = 2..16, liberation / bitmatrix, w = 16/32)
+// packet-bitsliced kernel for w = 2..16, liberation encode and syndrome
+// decode for w = 3, 5, 7, 11, 13 (one code object per w), w = 16/32)
 // on a scratch buffer; then the resources other threads' first calls would
 // create (profiles/r04_s11_threads.log: 67 ms for the first 1 MiB call of a
 // second thread, 4.5 ms for each later one): the batching queue of the
@@ -1532,11 +1561,17 @@ int warm_device(int dev) {
       std::vector<Warm> codes;
       for (int K = 1; K <= 16; ++K) codes.push_back({LEOEC_VANDRS, K, 1, 8});
       for (int w = 2; w <= 16; ++w) codes.push_back({LEOEC_CAUCHYRS, 2, 1, w});
-      codes.push_back({LEOEC_LIBERATION, 2, 2, 3});
+      for (int w : {3, 5, 7, 11, 13}) codes.push_back({LEOEC_LIBERATION, 2, 2, w});
       codes.push_back({LEOEC_VANDRS, 2, 1, 16});
       codes.push_back({LEOEC_VANDRS, 2, 1, 32});
-      for (const Warm& c : codes)
+      for (const Warm& c : codes) {
         (void)op_encode_dev(c.coding, c.k, c.m, c.w, d, kPar, 1024, 1, d + kPar, kPar, st->stream);
+        if (c.coding == LEOEC_LIBERATION) {  // the syndrome kernels' code objects (lib_inst.hip)
+          const int erased = 0;
+          (void)op_decode_dev(c.coding, c.k, c.m, c.w, d, kPar, 1024, 1, d + kPar, kPar, &erased,
+                              1, st->stream);
+        }
+      }
       (void)hipMemcpyAsync(h.data(), d + kPar, 4096, hipMemcpyDeviceToHost, st->stream);
     }
     (void)hipStreamSynchronize(st->stream);

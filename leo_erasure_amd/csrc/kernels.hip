@@ -155,6 +155,8 @@ uint32_t lib_lanes() {
 }
 template <int W>
 LibFn lib_kernel_w(int la) {
+  // (the product ships libb_apply from w = kLibbEncMinW: no lib_apply there)
+  if constexpr (!kMeasureBuild && W >= kLibbEncMinW) return nullptr;
 #ifdef LEOEC_MEASURE
   if (la == 4) return &detail::lib_apply<W, 4>;  // 256 lanes (lib_lanes())
   if (la == 8) return &detail::lib_apply<W, 8>;
@@ -309,8 +311,8 @@ using LibDecFn = void (*)(const detail::LibDecArgs);
 uint32_t lib_dec_lanes() { return kMeasureBuild && knobs().lib_dec_wg == 64 ? 64u : (uint32_t)kThreads; }
 LibbDec libb_dec(int w, int k) {
   const Knobs& kn = knobs();
-  const int la = kMeasureBuild ? kn.lib_dec_la : kLibbDecLA;
-  const int tw = kMeasureBuild ? kn.lib_dec_wg : kLibbDecTW;
+  const int la = kMeasureBuild && kn.lib_dec_la >= 0 ? kn.lib_dec_la : libb_dec_la(w);
+  const int tw = kMeasureBuild && kn.lib_dec_wg > 0 ? kn.lib_dec_wg : kLibbDecTW;
   switch (w) {
     case 3: return libb_dec_pick<3>(k, la, tw);
     case 5: return libb_dec_pick<5>(k, la, tw);
@@ -320,12 +322,15 @@ LibbDec libb_dec(int w, int k) {
     default: return {nullptr, 0};
   }
 }
+// (the round-1 syndrome kernel: measurement build only since round 5)
 template <int W>
 LibDecFn lib_dec_kernel_w() {
 #ifdef LEOEC_MEASURE
   if (lib_dec_lanes() == 64) return &detail::lib_dec_apply<W, 64>;
-#endif
   return &detail::lib_dec_apply<W>;
+#else
+  return nullptr;
+#endif
 }
 LibDecFn lib_dec_kernel(int w) {
   switch (w) {
@@ -340,19 +345,21 @@ LibDecFn lib_dec_kernel(int w) {
 }  // namespace
 
 bool lib_dec_supported(int w) {
-  return knobs().lib_form != 0 && lib_dec_kernel(w) != nullptr;
+  return knobs().lib_form != 0 && (w == 3 || w == 5 || w == 7 || w == 11 || w == 13);
 }
 
 int launch(const LibDecApply& p, hipStream_t s) {
   const int w = p.w;
-  LibDecFn fn = lib_dec_kernel(w);
-  uint32_t lanes = lib_dec_lanes();
-  if (knobs().lib_buf) {
+  LibDecFn fn = nullptr;
+  uint32_t lanes = 0;
+  if (knobs().lib_buf != 0) {  // shipped: libb_dec_apply
     const LibbDec b = libb_dec(w, p.k);
-    if (b.fn) {
-      fn = b.fn;
-      lanes = b.lanes;
-    }
+    fn = b.fn;
+    lanes = b.lanes;
+  }
+  if (!fn) {
+    fn = lib_dec_kernel(w);
+    lanes = lib_dec_lanes();
   }
   const int nout = (int)p.out.size();
   if (!fn || p.k <= 0 || p.k > w || (int)p.data.size() != p.k || p.cod.size() != 2 || nout < 1 ||
@@ -405,7 +412,8 @@ int launch(const BitApply& p, hipStream_t s) {
   if (p.block_size % ((uint64_t)16 * w) || p.block_size >= (1ull << 32)) return LEOEC_E_BAD_SIZE;
   if (!shards_ok(p.in) || !shards_ok(p.out)) return LEOEC_E_ARG;
   if (knobs().lib_form != 0 && is_liberation_encode(p)) {
-    if (knobs().lib_buf) {
+    const int buf = knobs().lib_buf;
+    if (buf > 0 || (buf < 0 && w >= kLibbEncMinW)) {
       const LibbEnc b = libb_enc(w, p.KB);
       if (b.fn) return launch_lib(p, b.fn, b.lanes, s);
     }

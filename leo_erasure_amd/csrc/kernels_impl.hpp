@@ -926,7 +926,7 @@ libb_apply(const LibArgs a) {
 template <int W, int K, int LA, bool FULL>
 __device__ __forceinline__ void libb_dec_tile(const LibDecArgs& a, uint64_t o64, uint32_t off,
                                               bool live) {
-  constexpr int RS = LA + 1, NB = K + 2, NP = NB * W;
+  constexpr int RS = LA + 1, NB = K + 2, NP = NB * W;  // LA = 0: the block form below
   uint32_t vo[W];
 #pragma unroll
   for (int x = 0; x < W; ++x) vo[x] = off + (uint32_t)x * a.ps;
@@ -942,33 +942,52 @@ __device__ __forceinline__ void libb_dec_tile(const LibDecArgs& a, uint64_t o64,
   u32x4 S[2 * W];  // P syndromes, then Q syndromes
 #pragma unroll
   for (int s = 0; s < 2 * W; ++s) S[s] = u32x4{0u, 0u, 0u, 0u};
-  u32x4 ring[RS];
-#pragma unroll
-  for (int q = 0; q < LA; ++q) ring[q] = libb_load(rs(q / W), vo[q % W]);
-#pragma unroll
-  for (int blk = 0; blk < NB; ++blk) {
+  auto eat = [&](int blk, int x, u32x4 v) {  // packet x of stream block blk
     const int j = blk - 2;
     const int y = j > 0 ? (j * ((W - 1) / 2)) % W : 0;
-#pragma unroll
-    for (int x = 0; x < W; ++x) {
-      const int p = blk * W + x, q = p + LA;
-      if (q < NP) ring[q % RS] = libb_load(rs(q / W), vo[q % W]);
-      u32x4 v = ring[p % RS];
-      if (!FULL) v = libb_clip(v, shard_of(blk).valid, vo[x]);
-      if (blk < 2) {
-        S[blk * W + x] ^= v;
-        libb_pin(S[blk * W + x]);
-      } else {
-        S[x] ^= v;
-        S[W + (x - j + W) % W] ^= v;
-        libb_pin(S[x]);
-        libb_pin(S[W + (x - j + W) % W]);
-        if (j > 0 && x == (y + j - 1) % W) {
-          S[W + y] ^= v;
-          libb_pin(S[W + y]);
-        }
+    if (!FULL) v = libb_clip(v, shard_of(blk).valid, vo[x]);
+    if (blk < 2) {
+      S[blk * W + x] ^= v;
+      libb_pin(S[blk * W + x]);
+    } else {
+      S[x] ^= v;
+      S[W + (x - j + W) % W] ^= v;
+      libb_pin(S[x]);
+      libb_pin(S[W + (x - j + W) % W]);
+      if (j > 0 && x == (y + j - 1) % W) {
+        S[W + y] ^= v;
+        libb_pin(S[W + y]);
       }
-      __builtin_amdgcn_sched_barrier(0);  // as libb_enc_tile
+    }
+    __builtin_amdgcn_sched_barrier(0);  // as libb_enc_tile
+  };
+  if constexpr (LA == 0) {
+    // block form: an absent shard (erased data block, coding block not a
+    // survivor) is skipped by a uniform branch instead of streamed as zeros
+    // (at k = 4 a third of the stream); a present block's w loads are in
+    // flight together, then consumed
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk) {
+      if (shard_of(blk).base == nullptr) continue;
+      const auto r = rs(blk);
+      u32x4 yv[W];
+#pragma unroll
+      for (int x = 0; x < W; ++x) yv[x] = libb_load(r, vo[x]);
+#pragma unroll
+      for (int x = 0; x < W; ++x) eat(blk, x, yv[x]);
+    }
+  } else {
+    u32x4 ring[RS];
+#pragma unroll
+    for (int q = 0; q < LA; ++q) ring[q] = libb_load(rs(q / W), vo[q % W]);
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk) {
+#pragma unroll
+      for (int x = 0; x < W; ++x) {
+        const int p = blk * W + x, q = p + LA;
+        if (q < NP) ring[q % RS] = libb_load(rs(q / W), vo[q % W]);
+        eat(blk, x, ring[p % RS]);
+      }
     }
   }
   if (!live) return;
@@ -1032,8 +1051,16 @@ struct LibbDec {
   LibbDecFn fn;
   uint32_t lanes;
 };
-constexpr int kLibbEncLA = 2, kLibbEncTW = 64;    // shipped encode form
-constexpr int kLibbDecLA = 2, kLibbDecTW = 256;   // shipped decode form
+// The shipped liberation forms (round 5; interleaved A/B on two boxes,
+// profiles/r05_s3_ab_lib_*.log, r05_s4_ab_lib_*.log):
+//  encode: libb_apply (look-ahead 2, 64 lanes) for w >= 11 (+1 to +6 %);
+//          lib_apply below (libb_apply -2 to -8 % at w <= 7);
+//  decode and repair through syndromes: libb_dec_apply with 64 lanes,
+//          look-ahead 4 at w = 13, 2 below (+5 to +16 % at w >= 7 with
+//          k >= 7, within +-1 % at (4,2,7) and (5,2,5)).
+constexpr int kLibbEncLA = 2, kLibbEncTW = 64, kLibbEncMinW = 11;
+constexpr int kLibbDecTW = 64;
+constexpr int libb_dec_la(int w) { return w >= 13 ? 4 : 2; }
 template <int W>
 LibbEnc libb_enc_pick(int k, int la, int tw);
 template <int W>

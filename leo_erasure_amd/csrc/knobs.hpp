@@ -65,11 +65,17 @@ struct Knobs {
   int lib_form = 1;          // LEOEC_LIB_FORM=0: liberation through the generic bitmatrix kernel
   int lib_la = 2;            // LEOEC_LIB_LA: lib_apply packet look-ahead
   int lib_wg = 64;           // LEOEC_LIB_WG=256: lib_apply with 256-lane workgroups (4 KiB tiles)
-  int lib_dec_wg = 256;      // LEOEC_LIB_DEC_WG=64: lib_dec_apply with 64-lane workgroups
+  int lib_dec_wg = 0;        // LEOEC_LIB_DEC_WG=64|256: the syndrome kernel's lanes (0: the
+                             //   form's shipped width, 64 libb_dec_apply / 256 lib_dec_apply)
   int lib_xmap = 2;          // LEOEC_LIB_XMAP=0: liberation kernels without xcd_obj_map
-  int lib_buf = 0;           // LEOEC_LIB_BUF=1: liberation encode / decode with branch-free raw
-                             //   buffer loads (libb_apply / libb_dec_apply, kernels_impl.hpp)
-  int lib_dec_la = 2;        // LEOEC_LIB_DEC_LA: libb_dec_apply packet look-ahead
+  int lib_buf = -1;          // LEOEC_LIB_BUF: the liberation kernels with branch-free raw buffer
+                             //   loads (libb_apply / libb_dec_apply, kernels_impl.hpp): -1 the
+                             //   shipped policy (encode w >= 11, every syndrome decode), 1 always,
+                             //   0 never (lib_apply / lib_dec_apply)
+  int lib_dec_la = -1;       // LEOEC_LIB_DEC_LA: libb_dec_apply packet look-ahead (0: the block
+                             //   form; -1: shipped, libb_dec_la(w))
+  int lib_dec_cod = 1;       // LEOEC_LIB_DEC_COD=0: wanted coding blocks (repair of {data, P},
+                             //   {Q}, ...) through the generic bitmatrix kernel, not syndromes
   // gfbit_inst.hip
   int gfbit_xmap = -1;       // LEOEC_GFBIT_XMAP: 0 off, 1 object-contiguous, unset auto
   int gfbit_lw = 2;          // LEOEC_GFBIT_LW: lane width (dwords per packet), w = 8

@@ -115,16 +115,16 @@ int launch(const LibDecApply& a, hipStream_t s) {
     BitMatrix B;
     if (liberation_coding_bitmatrix(k, w, &B)) return;
     const uint64_t ps = a.block_size / (uint64_t)w;
-    // syndromes of the surviving coding blocks: S = C ^ B_{C,S} D_S
+    // syndromes S_c = [c survives] C ^ B_{c,S} D_S for both coding blocks
+    // (an absent shard reads as zero, as in the GPU kernel)
     std::vector<std::vector<uint8_t>> syn((size_t)2 * w, std::vector<uint8_t>(ps));
     std::vector<uint8_t> acc(ps);
     for (uint64_t o = 0; o < a.nobj; ++o) {
       for (int c = 0; c < 2; ++c) {
-        if (!a.cod[c].base) continue;
         for (int r = 0; r < w; ++r) {
           std::vector<uint8_t>& sy = syn[(size_t)c * w + r];
           std::fill(sy.begin(), sy.end(), 0);
-          xor_packet(sy, a.cod[c], o, r, ps);
+          if (a.cod[c].base) xor_packet(sy, a.cod[c], o, r, ps);
           for (int j = 0; j < k; ++j)
             if (a.data[j].base)
               for (int x = 0; x < w; ++x)

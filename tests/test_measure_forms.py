@@ -128,6 +128,12 @@ def _liberation_roundtrips(le, oracle):
                 ids = list(range(2, k + 2))
                 st, rep = le.nif_repair("liberation", (k, 2, w), [blocks[i] for i in ids], ids, [1])
                 assert st == "ok" and rep == [blocks[1]], (k, w)
+            # syndrome repair of coding blocks (round 5): {data, P}, {data, Q},
+            # P alone, Q alone, from every other block
+            for want in ([0, k], [k - 1, k + 1], [k], [k + 1]):
+                ids = [i for i in range(k + 2) if i not in want]
+                st, rep = le.nif_repair("liberation", (k, 2, w), [blocks[i] for i in ids], ids, want)
+                assert st == "ok" and rep == [blocks[i] for i in want], (k, w, want)
 
 
 @pytest.mark.parametrize("k,w,size", [(7, 7, 300007), (4, 7, 1048576), (10, 11, 1048573)])

@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--size", type=int, default=1 << 20)
     ap.add_argument("--objects", type=int, default=1024)
     ap.add_argument("--erased", default="0,1,2,3")
+    ap.add_argument("--repair", default="",
+                    help="block ids rebuilt by a timed repair (leoec_repair_dev from the other "
+                         "blocks, outputs in one [n][r*bs] buffer); empty: no repair op")
     ap.add_argument("--variants", default="")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=20)
@@ -69,6 +72,15 @@ def main():
     if er:
         ops["decode%s" % er] = (lambda: le.device.decode(args.coding, p, objs, args.size, par, er),
                                 (k + e) * bs * n)
+    rep = [int(x) for x in args.repair.split(",") if x]
+    if rep:
+        blocks = [objs[:, j * bs:] if j < k else par[:, (j - k) * bs:] for j in range(k + m)]
+        for i in rep:
+            blocks[i] = None
+        rout = torch.zeros((n, len(rep) * bs), dtype=torch.uint8, device="cuda")
+        routs = [rout[:, r * bs:] for r in range(len(rep))]
+        ops["repair%s" % rep] = (lambda: le.device.repair(args.coding, p, blocks, bs, rep, routs, n),
+                                 (k + len(rep)) * bs * n)
     s = torch.cuda.current_stream()
     res = {(v, o): [] for v in variants for o in ops}
     ok = {}
@@ -79,10 +91,21 @@ def main():
             for i in er:  # clear the erased data blocks, then rebuild them
                 if i < k:
                     objs[:, i * bs:min((i + 1) * bs, args.size)] = 0
-            list(ops.values())[1][0]()
+            ops["decode%s" % er][0]()
         torch.cuda.synchronize()
         ok[v] = bool(torch.equal(objs[:, :args.size], ref))
         objs[:, :args.size].copy_(ref)
+        if rep:
+            rout.fill_(0x5A)
+            ops["repair%s" % rep][0]()
+            torch.cuda.synchronize()
+            for r, i in enumerate(rep):
+                src = objs[:, i * bs:(i + 1) * bs] if i < k else par[:, (i - k) * bs:(i - k + 1) * bs]
+                # a data block past the object's size reads as zero
+                want = src.clone()
+                if i < k:
+                    want[:, max(0, min(bs, args.size - i * bs)):] = 0
+                ok[v] = ok[v] and bool(torch.equal(rout[:, r * bs:(r + 1) * bs], want))
     for _ in range(args.rounds):
         for v in variants:
             setenv(v)

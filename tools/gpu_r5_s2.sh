@@ -3,7 +3,9 @@
 # libb_dec_apply, measurement build, LEOEC_LIB_BUF=1): every GPU test (the new
 # forms in the measurement child), then interleaved A/B against the shipped
 # lib_apply / lib_dec_apply on liberation (7,2,7), (4,2,7), (10,2,11) at
-# 1,024 x 1 MiB, then the issue counters of the new forms and of repair.
+# 1,024 x 1 MiB, liberation's XOR-only access-pattern ceiling
+# (tools/lib_ceiling.hip), then the issue counters of the new forms and of
+# repair.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p $OUT
@@ -11,6 +13,8 @@ step() { local name=$1 t=$2; shift 2; echo "=== $name"; timeout -k 10 "$t" "$@" 
 step r05_s2_smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step r05_s2_pytest 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread
 cp $OUT/measure_forms.log $OUT/r05_s2_measure_forms.log
+TAILN=16 step r05_s2_lib_ceiling_727 300 tools/lib_ceiling 1024 20 7
+TAILN=16 step r05_s2_lib_ceiling_427 300 tools/lib_ceiling 1024 20 4
 V=";LEOEC_LIB_BUF=1;LEOEC_LIB_BUF=1,LEOEC_LIB_LA=4;LEOEC_LIB_BUF=1,LEOEC_LIB_LA=8;LEOEC_LIB_BUF=1,LEOEC_LIB_WG=256;LEOEC_LIB_BUF=1,LEOEC_LIB_DEC_LA=4;LEOEC_LIB_BUF=1,LEOEC_LIB_DEC_WG=64;LEOEC_LIB_BUF=1,LEOEC_LIB_DEC_WG=64,LEOEC_LIB_DEC_LA=4"
 TAILN=16 step r05_s2_ab_lib727 600 python tools/env_ab.py --coding liberation --k 7 --m 2 --w 7 --erased 0,1 --objects 1024 --rounds 4 --variants "$V"
 TAILN=16 step r05_s2_ab_lib427 600 python tools/env_ab.py --coding liberation --k 4 --m 2 --w 7 --erased 0,1 --objects 1024 --rounds 4 --variants "$V"

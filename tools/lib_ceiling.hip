@@ -1,0 +1,296 @@
+// lib_ceiling.hip — measurement only (not part of the engine): the memory
+// ceiling of the liberation(k,2,w) encode's ACCESS PATTERN on the
+// reference's 1 MiB geometry (round-5 verdict item 1).  liberation(7,2,7):
+// block bs = 149,856 B = 7 packets of ps = 21,408 B (167.25 cache lines:
+// packet x of block j starts 32 * ((7 j + x) mod 4) bytes into a 128-B
+// line), objects in rows of k * bs, P and Q in their own buffer.
+//
+// Every form reads each input packet once and writes each output packet
+// once, 16 bytes per lane, XOR instead of the liberation structure (every
+// input packet x of every block into P[x] and Q[x]), so the arithmetic is
+// nothing; the forms differ in how loads are issued:
+//   branchy  the shipped lib_apply's shape: a per-load uniform branch
+//            between a plain load and a guarded one (every load then waits
+//            for all outstanding loads), packet ring of LA
+//   ring     raw buffer loads, no branch, LA packets in flight (libb_apply)
+//   block    raw buffer loads, a whole block (w packets) in flight
+//   copy     a plain streaming copy-and-XOR of the same bytes: each lane
+//            reads its 16 B of the k data blocks' flat rows and writes 2
+//            blocks' worth, no packet structure (the part's rate for this
+//            byte count)
+// on the reference geometry and on objects sized so packets are line
+// aligned (ps = 21,504 B), at 64 and 256 lanes per workgroup.
+//
+//   hipcc --offload-arch=gfx950 -O3 -o tools/lib_ceiling tools/lib_ceiling.hip
+//   tools/lib_ceiling [objects] [reps] [k]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <functional>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#define CHECK(x)                                                                \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+constexpr int W = 7;
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+
+struct Geo {
+  unsigned ps, bs, tiles, k;
+  unsigned long long row;  // object row bytes (k * bs)
+  unsigned full_tiles;     // tiles wholly inside the packet
+};
+
+__device__ __forceinline__ unsigned obj_map(unsigned b, unsigned n, unsigned tiles) {
+  const unsigned full = (n / tiles / 8u) * 8u * tiles;
+  if (b >= full) return b;
+  const unsigned x = b % 8u, i = b / 8u;
+  return ((i / tiles) * 8u + x) * tiles + i % tiles;
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, n, 0x00020000);
+}
+__device__ __forceinline__ void pin(u4& v) { asm volatile("" : "+v"(v)); }
+
+// FORM 0 branchy, 1 ring, 2 block.  K compiled in (the engine's libb form).
+template <int K, int FORM, int LA, int TW>
+__global__ void __launch_bounds__(TW) __attribute__((amdgpu_waves_per_eu(4, 8)))
+pattern(const unsigned char* __restrict__ in, unsigned char* __restrict__ out, Geo g) {
+  const unsigned b = obj_map(blockIdx.x, gridDim.x, g.tiles);
+  const unsigned obj = b / g.tiles, tile = b % g.tiles;
+  const unsigned t0 = tile * TW * 16u, off = t0 + threadIdx.x * 16u;
+  const bool full = tile < g.full_tiles;  // wave-uniform
+  const unsigned char* ib = in + (size_t)obj * g.row;
+  unsigned char* ob = out + (size_t)obj * 2 * g.bs;
+  u4 P[W], Q[W];
+  for (int x = 0; x < W; ++x) P[x] = Q[x] = u4{0u, 0u, 0u, 0u};
+  auto load = [&](int q) -> u4 {
+    const int j = q / W, x = q % W;
+    const unsigned pos = (unsigned)x * g.ps + off;
+    if constexpr (FORM == 0) {
+      const unsigned char* p = ib + (size_t)j * g.bs + pos;
+      if (full) return __builtin_nontemporal_load(reinterpret_cast<const u4*>(p));
+      u4 v = {0u, 0u, 0u, 0u};
+      if (off < g.ps) v = __builtin_nontemporal_load(reinterpret_cast<const u4*>(p));
+      return v;
+    } else {
+      return __builtin_amdgcn_raw_buffer_load_b128(rsrc(ib + (size_t)j * g.bs, g.bs), pos, 0, 2);
+    }
+  };
+  auto eat = [&](int q, u4 v) {
+    const int x = q % W;
+    P[x] ^= v;
+    Q[x] ^= v;
+    if constexpr (FORM != 0) {
+      pin(P[x]);
+      pin(Q[x]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  constexpr int NP = K * W;
+  if constexpr (FORM == 2) {
+    u4 y[2][W];
+#pragma unroll
+    for (int x = 0; x < W; ++x) y[0][x] = load(x);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (j + 1 < K)
+#pragma unroll
+        for (int x = 0; x < W; ++x) y[(j + 1) & 1][x] = load((j + 1) * W + x);
+#pragma unroll
+      for (int x = 0; x < W; ++x) eat(j * W + x, y[j & 1][x]);
+    }
+  } else {
+    constexpr int RS = LA + 1;
+    u4 ring[RS];
+#pragma unroll
+    for (int q = 0; q < LA; ++q) ring[q] = load(q);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      if (p + LA < NP) ring[(p + LA) % RS] = load(p + LA);
+      eat(p, ring[p % RS]);
+    }
+  }
+  if (off >= g.ps) return;
+#pragma unroll
+  for (int x = 0; x < W; ++x) {
+    unsigned char* p = ob + (size_t)x * g.ps + off;
+    __builtin_nontemporal_store(P[x], reinterpret_cast<u4*>(p));
+    __builtin_nontemporal_store(Q[x], reinterpret_cast<u4*>(p + g.bs));
+  }
+}
+
+// A flat streaming kernel over the same bytes: lane l of tile t reads 16 B
+// at t * TW * 16 + l * 16 of each of the K data blocks (blocks as flat
+// rows, no packets) and writes the XOR to both output blocks.
+template <int K, int TW>
+__global__ void __launch_bounds__(TW) __attribute__((amdgpu_waves_per_eu(4, 8)))
+flat(const unsigned char* __restrict__ in, unsigned char* __restrict__ out, Geo g,
+     unsigned ftiles) {
+  const unsigned b = obj_map(blockIdx.x, gridDim.x, ftiles);
+  const unsigned obj = b / ftiles, tile = b % ftiles;
+  const unsigned off = tile * TW * 16u + threadIdx.x * 16u;
+  if (off >= g.bs) return;
+  const unsigned char* ib = in + (size_t)obj * g.row;
+  u4 a = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    a ^= __builtin_nontemporal_load(reinterpret_cast<const u4*>(ib + (size_t)j * g.bs + off));
+  unsigned char* ob = out + (size_t)obj * 2 * g.bs;
+  __builtin_nontemporal_store(a, reinterpret_cast<u4*>(ob + off));
+  __builtin_nontemporal_store(a, reinterpret_cast<u4*>(ob + g.bs + off));
+}
+
+__global__ void fill_random(unsigned* p, size_t n, unsigned seed) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    unsigned long long z = (i + seed) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    p[i] = (unsigned)(z ^ (z >> 31));
+  }
+}
+
+typedef void (*KFn)(const unsigned char*, unsigned char*, Geo);
+struct Case {
+  std::string name;
+  KFn k;
+  unsigned tw;
+  bool aligned;
+};
+
+template <int K>
+int run(unsigned nobj, int reps) {
+  // liberation geometry (engine op_layout): bs = ceil16(ceil(N / (k w))) * w
+  auto geo = [&](unsigned long long osz) {
+    Geo g{};
+    const unsigned long long per = (osz + (unsigned long long)K * W - 1) / ((unsigned long long)K * W);
+    g.bs = (unsigned)((per + 15) / 16 * 16 * W);
+    g.ps = g.bs / W;
+    g.k = K;
+    g.row = (unsigned long long)K * g.bs;
+    return g;
+  };
+  const Geo ref = geo(1ull << 20);
+  // line-aligned packets: ps rounded up to 128
+  const unsigned long long apacket = (ref.ps + 127) / 128 * 128;
+  const Geo ali = geo(apacket * W * K);
+  printf("# liberation(%d,2,%d), %u objects: ps %u (mod 128 = %u), aligned ps %u (mod 128 = %u)\n",
+         K, W, nobj, ref.ps, ref.ps % 128, ali.ps, ali.ps % 128);
+  const size_t in_bytes = (size_t)nobj * ali.row + 4096, out_bytes = (size_t)nobj * 2 * ali.bs + 4096;
+  unsigned char *in, *out, *out2;
+  CHECK(hipMalloc(&in, in_bytes));
+  CHECK(hipMalloc(&out, out_bytes));
+  CHECK(hipMalloc(&out2, out_bytes));
+  hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, (unsigned*)in, in_bytes / 4, 7u);
+  CHECK(hipDeviceSynchronize());
+#define PC(F, LA, TW) reinterpret_cast<KFn>(&pattern<K, F, LA, TW>)
+  std::vector<Case> cases = {
+      {"branchy la2 wg64 (shipped lib_apply's load shape)", PC(0, 2, 64), 64, false},
+      {"ring la2 wg64 (libb_apply)", PC(1, 2, 64), 64, false},
+      {"ring la4 wg64", PC(1, 4, 64), 64, false},
+      {"ring la8 wg64", PC(1, 8, 64), 64, false},
+      {"block wg64", PC(2, 0, 64), 64, false},
+      {"ring la2 wg256", PC(1, 2, 256), 256, false},
+      {"ring la4 wg256", PC(1, 4, 256), 256, false},
+      {"block wg256", PC(2, 0, 256), 256, false},
+      {"branchy la2 wg64, aligned packets", PC(0, 2, 64), 64, true},
+      {"ring la2 wg64, aligned packets", PC(1, 2, 64), 64, true},
+      {"ring la4 wg64, aligned packets", PC(1, 4, 64), 64, true},
+      {"block wg64, aligned packets", PC(2, 0, 64), 64, true},
+  };
+  // every packet form computes the same XORs: outputs compared with the
+  // first form's, byte for byte, on the reference geometry
+  {
+    std::vector<unsigned char> a(out_bytes), b(out_bytes);
+    for (size_t c = 0; c < cases.size(); ++c) {
+      if (cases[c].aligned) continue;
+      Geo g = ref;
+      g.tiles = (g.ps + cases[c].tw * 16 - 1) / (cases[c].tw * 16);
+      g.full_tiles = g.ps / (cases[c].tw * 16);
+      CHECK(hipMemset(out, 0, out_bytes));
+      hipLaunchKernelGGL(cases[c].k, dim3(nobj * g.tiles), dim3(cases[c].tw), 0, 0, in, out, g);
+      CHECK(hipMemcpy(c == 0 ? a.data() : b.data(), out, out_bytes, hipMemcpyDeviceToHost));
+      if (c && a != b) {
+        printf("# form %s: output differs from the branchy form\n", cases[c].name.c_str());
+        return 3;
+      }
+    }
+    printf("# every reference-geometry form wrote the same bytes\n");
+  }
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  std::vector<std::vector<float>> t(cases.size() + 2);
+  for (int round = 0; round < 4; ++round) {
+    for (size_t c = 0; c < cases.size() + 2; ++c) {
+      Geo g = c < cases.size() && cases[c].aligned ? ali : ref;
+      std::function<void()> launch;
+      if (c < cases.size()) {
+        g.tiles = (g.ps + cases[c].tw * 16 - 1) / (cases[c].tw * 16);
+        g.full_tiles = g.ps / (cases[c].tw * 16);
+        const KFn k = cases[c].k;
+        const unsigned tw = cases[c].tw;
+        launch = [=]() { hipLaunchKernelGGL(k, dim3(nobj * g.tiles), dim3(tw), 0, 0, in, out, g); };
+      } else {
+        const unsigned tw = c == cases.size() ? 64 : 256;
+        const unsigned ft = (g.bs + tw * 16 - 1) / (tw * 16);
+        launch = [=]() {
+          if (tw == 64) hipLaunchKernelGGL((flat<K, 64>), dim3(nobj * ft), dim3(64), 0, 0, in, out2, g, ft);
+          else hipLaunchKernelGGL((flat<K, 256>), dim3(nobj * ft), dim3(256), 0, 0, in, out2, g, ft);
+        };
+      }
+      {  // time-based warm-up: the clock ramps over the first milliseconds
+        CHECK(hipEventRecord(e0, 0));
+        float ms = 0.f;
+        while (ms < 300.f) {
+          for (int i = 0; i < 10; ++i) launch();
+          CHECK(hipEventRecord(e1, 0));
+          CHECK(hipEventSynchronize(e1));
+          CHECK(hipEventElapsedTime(&ms, e0, e1));
+        }
+      }
+      for (int i = 0; i < reps; ++i) {
+        CHECK(hipEventRecord(e0, 0));
+        launch();
+        CHECK(hipEventRecord(e1, 0));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        t[c].push_back(ms);
+      }
+    }
+  }
+  CHECK(hipGetLastError());
+  for (size_t c = 0; c < cases.size() + 2; ++c) {
+    std::sort(t[c].begin(), t[c].end());
+    const double ms = t[c][t[c].size() / 2];
+    const Geo g = c < cases.size() && cases[c].aligned ? ali : ref;
+    const double bytes = (double)nobj * (K + 2) * g.bs;
+    const std::string name = c < cases.size() ? cases[c].name
+                             : c == cases.size() ? "flat copy-xor wg64 (same bytes, no packets)"
+                                                 : "flat copy-xor wg256 (same bytes, no packets)";
+    printf("{\"k\": %d, \"case\": \"%s\", \"ms_med\": %.4f, \"frac\": %.4f}\n", K, name.c_str(), ms,
+           bytes / ms / 1e6 / 8000.0);
+  }
+  CHECK(hipFree(in));
+  CHECK(hipFree(out));
+  CHECK(hipFree(out2));
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  const unsigned nobj = argc > 1 ? (unsigned)atoi(argv[1]) : 1024u;
+  const int reps = argc > 2 ? atoi(argv[2]) : 20;
+  const int k = argc > 3 ? atoi(argv[3]) : 7;
+  if (k == 4) return run<4>(nobj, reps);
+  return run<7>(nobj, reps);
+}
