@@ -311,7 +311,7 @@ using LibDecFn = void (*)(const detail::LibDecArgs);
 uint32_t lib_dec_lanes() { return kMeasureBuild && knobs().lib_dec_wg == 64 ? 64u : (uint32_t)kThreads; }
 LibbDec libb_dec(int w, int k) {
   const Knobs& kn = knobs();
-  const int la = kMeasureBuild && kn.lib_dec_la >= 0 ? kn.lib_dec_la : libb_dec_la(w);
+  const int la = kMeasureBuild && kn.lib_dec_la >= 0 ? kn.lib_dec_la : libb_dec_la(w, k);
   const int tw = kMeasureBuild && kn.lib_dec_wg > 0 ? kn.lib_dec_wg : kLibbDecTW;
   switch (w) {
     case 3: return libb_dec_pick<3>(k, la, tw);

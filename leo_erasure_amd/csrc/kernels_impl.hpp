@@ -1056,11 +1056,12 @@ struct LibbDec {
 //  encode: libb_apply (look-ahead 2, 64 lanes) for w >= 11 (+1 to +6 %);
 //          lib_apply below (libb_apply -2 to -8 % at w <= 7);
 //  decode and repair through syndromes: libb_dec_apply with 64 lanes,
-//          look-ahead 4 at w = 13, 2 below (+5 to +16 % at w >= 7 with
-//          k >= 7, within +-1 % at (4,2,7) and (5,2,5)).
+//          look-ahead 4 at w = 13 or k <= 4, 2 otherwise (+5 to +16 % at
+//          w >= 7 with k >= 7, +2 % at (4,2,7) with look-ahead 4, within
+//          +-4 % at (5,2,5)).
 constexpr int kLibbEncLA = 2, kLibbEncTW = 64, kLibbEncMinW = 11;
 constexpr int kLibbDecTW = 64;
-constexpr int libb_dec_la(int w) { return w >= 13 ? 4 : 2; }
+constexpr int libb_dec_la(int w, int k) { return (w >= 13 || k <= 4) ? 4 : 2; }
 template <int W>
 LibbEnc libb_enc_pick(int k, int la, int tw);
 template <int W>

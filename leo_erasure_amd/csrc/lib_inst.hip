@@ -27,7 +27,6 @@ constexpr bool kMeasureBuildTU = true;
 constexpr bool kMeasureBuildTU = false;
 #endif
 
-constexpr int kDecLA = libb_dec_la(kW);
 // libb_apply is shipped for w >= kLibbEncMinW only; the measurement build
 // has it at every w (LEOEC_LIB_BUF=1 forces it, A/B and parity)
 constexpr bool kEncBuilt = kMeasureBuildTU || kW >= kLibbEncMinW;
@@ -46,7 +45,8 @@ LibbEnc enc_shipped(std::index_sequence<I...>, int k) {
 template <std::size_t... I>
 LibbDec dec_shipped(std::index_sequence<I...>, int k) {
   static const LibbDec tbl[] = {
-      {&libb_dec_apply<kW, (int)I + 1, kDecLA, kLibbDecTW>, (uint32_t)kLibbDecTW}...};
+      {&libb_dec_apply<kW, (int)I + 1, libb_dec_la(kW, (int)I + 1), kLibbDecTW>,
+       (uint32_t)kLibbDecTW}...};
   return tbl[k - 1];
 }
 
@@ -108,7 +108,7 @@ template <>
 LibbDec libb_dec_pick<kW>(int k, int la, int tw) {
   if (k < 1 || k > kW) return {nullptr, 0};
 #ifdef LEOEC_MEASURE
-  if (la != kDecLA || tw != kLibbDecTW) {
+  if (la != libb_dec_la(kW, k) || tw != kLibbDecTW) {
     if constexpr (kW == 7) {
       if (k == 4) return dec_form<4>(la, tw);
       if (k == 7) return dec_form<7>(la, tw);
