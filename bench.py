@@ -316,13 +316,41 @@ class GpuBackend:
             enc_ok, dec_ok = check()
         finally:
             le._lib.host_spread([])
+        link = self.link_h2d()
+        # each encode moves its object's bytes host -> device, a decode its 10
+        # survivor blocks: the H2D direction bounds both (D2H runs beside it)
+        h2d_enc = enc_gibs * 2**30 * 1.0 / 1e9
+        h2d_dec = dec_gibs * 2**30 * (K * bs / size) / 1e9
         return {"encode_GiBps": round(enc_gibs, 2), "decode_GiBps": round(dec_gibs, 2),
                 "callers": n, "seconds_per_op": seconds, "calls": [enc_calls, dec_calls],
+                "link_h2d_GBps": round(link, 1),
+                "h2d_over_link": {"encode": round(h2d_enc / link, 3) if link else None,
+                                  "decode": round(h2d_dec / link, 3) if link else None},
                 "parity_vs_gpu": {"objects": n, "encode_equal": enc_ok, "decode_equal": dec_ok},
                 "what": f"C ABI leoec_encode / leoec_decode (data blocks {ERASED} lost) of "
                         f"{size} B host objects from {n} threads, PCIe-inclusive "
                         "(pageable caller buffers; batching queue), this rank's device; "
                         "GiB/s of object payload"}
+
+
+    def link_h2d(self, mib=256, reps=5):
+        """This device's host -> device copy rate from pinned memory (one
+        `mib` MiB copy, median of `reps`, GB/s): the PCIe link the host
+        path's H2D direction runs on."""
+        t = self.torch
+        src = t.empty(mib << 20, dtype=t.uint8, pin_memory=True)
+        dst = t.empty(mib << 20, dtype=t.uint8, device=self.device)
+        ms = []
+        for i in range(reps + 1):
+            a, b = self.event(), self.event()
+            a.record()
+            dst.copy_(src, non_blocking=True)
+            b.record()
+            self.sync()
+            if i:
+                ms.append(a.elapsed_time(b))
+        del src, dst
+        return (mib << 20) / (sorted(ms)[len(ms) // 2] * 1e-3) / 1e9
 
 
 def pattern_child(args):
