@@ -316,16 +316,20 @@ class GpuBackend:
             enc_ok, dec_ok = check()
         finally:
             le._lib.host_spread([])
-        link = self.link_h2d()
-        # each encode moves its object's bytes host -> device, a decode its 10
-        # survivor blocks: the H2D direction bounds both (D2H runs beside it)
-        h2d_enc = enc_gibs * 2**30 * 1.0 / 1e9
-        h2d_dec = dec_gibs * 2**30 * (K * bs / size) / 1e9
+        link = self.link_rates()
+        # Bytes each op moves per payload byte: an encode its object host ->
+        # device and its m parity blocks back, a decode its K survivor blocks
+        # in and its rebuilt blocks back.  `link_busy` = the share of each
+        # second those bytes keep the link busy at the copy rates measured
+        # alone (H2D then D2H); near 1 means the op runs at the link.
+        e = len(ERASED)
+        per = {"encode": (1.0, M * bs / size), "decode": (K * bs / size, e * bs / size)}
+        rate = {"encode": enc_gibs, "decode": dec_gibs}
+        busy = {op: round(rate[op] * 2**30 / 1e9 * (h / link["h2d_GBps"] + d / link["d2h_GBps"]), 3)
+                for op, (h, d) in per.items()}
         return {"encode_GiBps": round(enc_gibs, 2), "decode_GiBps": round(dec_gibs, 2),
                 "callers": n, "seconds_per_op": seconds, "calls": [enc_calls, dec_calls],
-                "link_h2d_GBps": round(link, 1),
-                "h2d_over_link": {"encode": round(h2d_enc / link, 3) if link else None,
-                                  "decode": round(h2d_dec / link, 3) if link else None},
+                "link": link, "link_busy": busy,
                 "parity_vs_gpu": {"objects": n, "encode_equal": enc_ok, "decode_equal": dec_ok},
                 "what": f"C ABI leoec_encode / leoec_decode (data blocks {ERASED} lost) of "
                         f"{size} B host objects from {n} threads, PCIe-inclusive "
@@ -333,24 +337,43 @@ class GpuBackend:
                         "GiB/s of object payload"}
 
 
-    def link_h2d(self, mib=256, reps=5):
-        """This device's host -> device copy rate from pinned memory (one
-        `mib` MiB copy, median of `reps`, GB/s): the PCIe link the host
-        path's H2D direction runs on."""
+    def link_rates(self, mib=256, reps=5):
+        """This device's PCIe copy rates from / to pinned host memory (GB/s,
+        median of `reps` copies of `mib` MiB): host -> device alone, device
+        -> host alone, and both directions at once on two streams (bytes of
+        both / time) — the link the host-memory leg runs on."""
         t = self.torch
-        src = t.empty(mib << 20, dtype=t.uint8, pin_memory=True)
-        dst = t.empty(mib << 20, dtype=t.uint8, device=self.device)
-        ms = []
-        for i in range(reps + 1):
-            a, b = self.event(), self.event()
-            a.record()
-            dst.copy_(src, non_blocking=True)
-            b.record()
-            self.sync()
-            if i:
-                ms.append(a.elapsed_time(b))
-        del src, dst
-        return (mib << 20) / (sorted(ms)[len(ms) // 2] * 1e-3) / 1e9
+        n = mib << 20
+        hsrc = t.empty(n, dtype=t.uint8, pin_memory=True)
+        hdst = t.empty(n, dtype=t.uint8, pin_memory=True)
+        dsrc = t.empty(n, dtype=t.uint8, device=self.device)
+        ddst = t.empty(n, dtype=t.uint8, device=self.device)
+        cur = t.cuda.current_stream(self.device)
+        up, down = t.cuda.Stream(device=self.device), t.cuda.Stream(device=self.device)
+
+        def timed(h2d, d2h):
+            ms = []
+            for i in range(reps + 1):
+                a, b = self.event(), self.event()
+                a.record(cur)
+                for on, s, dst, src in ((h2d, up, ddst, hsrc), (d2h, down, hdst, dsrc)):
+                    if on:
+                        s.wait_stream(cur)
+                        with t.cuda.stream(s):
+                            dst.copy_(src, non_blocking=True)
+                        cur.wait_stream(s)
+                b.record(cur)
+                self.sync()
+                if i:
+                    ms.append(a.elapsed_time(b))
+            return (h2d + d2h) * n / (sorted(ms)[len(ms) // 2] * 1e-3) / 1e9
+
+        out = {"h2d_GBps": round(timed(True, False), 1), "d2h_GBps": round(timed(False, True), 1),
+               "both_GBps": round(timed(True, True), 1),
+               "what": f"pinned {mib} MiB copies, median of {reps}; both = the two directions "
+                       "at once on two streams, bytes of both / time"}
+        del hsrc, hdst, dsrc, ddst
+        return out
 
 
 def pattern_child(args):
