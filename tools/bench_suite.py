@@ -88,14 +88,24 @@ def stripe_case(torch, le, cls, k, m, w, size, n, reps, erased, repair_ids, name
         def blk(b):
             return objs[:, b * bs:] if b < k else parity[:, (b - k) * bs:]
         blocks = [None if b in repair_ids else blk(b) for b in range(k + m)]
-        outs = [torch.empty((n, bs), dtype=torch.uint8, device="cuda") for _ in repair_ids]
-        rep = lambda: le.device.repair(cls, (k, m, w), blocks, bs, repair_ids, outs, n)  # noqa
-        t_rep = timed(torch, rep, reps)
-        out.append(row(name, "repair%s" % repair_ids, t_rep, (k + len(repair_ids)) * bs * n,
-                       len(repair_ids) * bs * n, extra))
-        if verify:
-            for i, b in enumerate(repair_ids):
-                assert torch.equal(outs[i], blk(b)[:, :bs]), f"{name}: repair {b}"
+        r = len(repair_ids)
+        # outputs per object, one [n, r*bs] buffer (as encode's parity), and
+        # as r separate [n, bs] tensors: the same launch reads 4-5 % slower
+        # into separate tensors (profiles/r05_s7_repair_probe.log,
+        # r05_s8_repair_probe.log; not the HBM address aliasing of their
+        # 2 MiB-aligned bases: end to end in one buffer reads the same)
+        rows = torch.empty((n, r * bs), dtype=torch.uint8, device="cuda")
+        forms = [("per-object rows", [rows[:, i * bs:] for i in range(r)]),
+                 ("separate tensors", [torch.empty((n, bs), dtype=torch.uint8, device="cuda")
+                                       for _ in repair_ids])]
+        for form, outs in forms:
+            rep = lambda: le.device.repair(cls, (k, m, w), blocks, bs, repair_ids, outs, n)  # noqa
+            t_rep = timed(torch, rep, reps)
+            out.append(row(name, "repair%s" % repair_ids, t_rep, (k + r) * bs * n, r * bs * n,
+                           dict(extra, repair_out=form)))
+            if verify:
+                for i, b in enumerate(repair_ids):
+                    assert torch.equal(outs[i][:, :bs], blk(b)[:, :bs]), f"{name}: repair {b}"
     return out
 
 
