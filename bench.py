@@ -152,8 +152,9 @@ class GpuBackend:
         workgroups; measurement library `leoec_measure_xor_pattern_dev`,
         csrc/xor_pattern.hip, not a code), timed in alternating rounds with
         the shipped encode; (2) a device-to-device copy of the batch (torch
-        copy_, read + write bytes).  Overwrites `parity`.  Median per-launch
-        times."""
+        copy_, read + write bytes); (3) the pattern's reads alone and its
+        writes alone, timed in the same rounds (`halves`).  Overwrites
+        `parity`.  Median per-launch times."""
         import ctypes
         import os
         import statistics
@@ -183,12 +184,36 @@ class GpuBackend:
             self.sync()
             return [ev[i].elapsed_time(ev[i + 1]) for i in range(reps)]
 
-        times = {"shipped": [], "pattern": []}
+        def half(h):
+            def go():
+                rc = mlib.leoec_measure_stream_half_dev(
+                    h, objs.data_ptr(), objs.stride(0), size, n, parity.data_ptr(),
+                    parity.stride(0), ctypes.c_void_p(stream))
+                if rc != 0:
+                    raise RuntimeError(f"leoec_measure_stream_half_dev({h}) -> {rc}")
+            return go
+
+        times = {"shipped": [], "pattern": [], "reads": [], "writes": []}
         for _ in range(rounds):
             times["shipped"] += timed(lambda: self.encode(objs, size, parity))
             times["pattern"] += timed(xor_pattern)
-        ship = enc_bytes / (statistics.median(times["shipped"]) * 1e-3) / 1e9
-        patt = enc_bytes / (statistics.median(times["pattern"]) * 1e-3) / 1e9
+            times["reads"] += timed(half(0))
+            times["writes"] += timed(half(1))
+        med = {k: statistics.median(v) for k, v in times.items()}
+        ship = enc_bytes / (med["shipped"] * 1e-3) / 1e9
+        patt = enc_bytes / (med["pattern"] * 1e-3) / 1e9
+        # the encode's bytes split as its reads (K blocks) and writes (M)
+        rd_bytes, wr_bytes = enc_bytes * K // (K + M), enc_bytes * M // (K + M)
+        serial = enc_bytes / ((med["reads"] + med["writes"]) * 1e-3) / 1e9
+        halves = {"what": "the pattern's reads alone and its writes alone "
+                          "(leoec_measure_stream_half_dev); `serial` = the encode's bytes at "
+                          "those two rates back to back, an upper bound for a kernel that "
+                          "mixes them (HBM read/write turnarounds)",
+                  "reads_achieved": round(rd_bytes / (med["reads"] * 1e-3) / 1e9, 1),
+                  "writes_achieved": round(wr_bytes / (med["writes"] * 1e-3) / 1e9, 1),
+                  "serial_achieved": round(serial, 1),
+                  "serial_frac": round(serial / HBM_PEAK_GBS, 4),
+                  "shipped_over_serial": round(ship / serial, 4)}
         dst = self.torch.empty_like(objs)
         copy_ms = statistics.median(timed(lambda: dst.copy_(objs)))
         del dst
@@ -203,6 +228,7 @@ class GpuBackend:
                                  "read + write bytes", "bytes": copy_bytes,
                          "achieved": round(copy, 1), "frac": round(copy / HBM_PEAK_GBS, 4)},
                 "shipped_over_copy": round(ship / copy, 4),
+                "halves": halves,
                 "sample": f"{rounds} alternating rounds x {reps} launches each, medians"}
 
 

@@ -100,6 +100,11 @@ def _load(path=LIB_PATH):
             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
             ctypes.c_uint64, ctypes.c_void_p]
         L.leoec_measure_xor_pattern_dev.restype = ctypes.c_int
+    if hasattr(L, "leoec_measure_stream_half_dev"):
+        L.leoec_measure_stream_half_dev.argtypes = [
+            ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        L.leoec_measure_stream_half_dev.restype = ctypes.c_int
     _loaded[path] = L
     return L
 

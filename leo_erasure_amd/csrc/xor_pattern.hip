@@ -63,21 +63,83 @@ __global__ void __launch_bounds__(kLanes) xor_pattern(const XorArgs a) {
   }
 }
 
+// The two halves of that traffic alone (round 5, tools/hbm_mix.hip): READS
+// loads the 10 data columns as xor_pattern does and stores nothing (their
+// XOR is stored only if it equals a value random data does not produce);
+// WRITES stores the 4 parity columns (a pattern of lane, object and offset)
+// and loads nothing.  The encode's bytes at the part's read rate plus its
+// write rate (the two back to back) bound an encode that reads and writes
+// at once from above: mixing them costs HBM read/write turnarounds.
+template <bool READS>
+__global__ void __launch_bounds__(kLanes) stream_half(const XorArgs a, uint32_t never) {
+  const uint32_t obj = blockIdx.x / a.tiles;
+  const uint32_t off = (blockIdx.x - obj * a.tiles) * (kLanes * 16u) + threadIdx.x * 16u;
+  if (off >= a.bs) return;
+  uint8_t* ob = a.parity + (uint64_t)obj * a.pstride;
+  if (READS) {
+    const uint8_t* ib = a.objs + (uint64_t)obj * a.stride;
+    u32x4 d[kK];
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+      const uint32_t lo = (uint32_t)j * a.bs;
+      const uint32_t valid = a.size > lo ? (a.size - lo < a.bs ? a.size - lo : a.bs) : 0u;
+      d[j] = __builtin_amdgcn_raw_buffer_load_b128(range(ib + lo, valid), off, 0, 2);
+    }
+    u32x4 acc = d[0];
+#pragma unroll
+    for (int j = 1; j < kK; ++j) acc ^= d[j];
+    if (acc[0] == never && acc[1] == never && acc[2] == never && acc[3] == never)
+      __builtin_amdgcn_raw_buffer_store_b128(acc, range(ob, a.bs), off, 0, 2);
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    const u32x4 v = {threadIdx.x, obj, off, (uint32_t)r};
+    __builtin_amdgcn_raw_buffer_store_b128(v, range(ob + (uint64_t)r * a.bs, a.bs), off, 0, 2);
+  }
+}
+
+bool xor_args(const uint8_t* objs, uint64_t stride, uint64_t size, uint64_t nobj, uint8_t* parity,
+              uint64_t pstride, XorArgs* a, uint32_t* grid) {
+  if (!objs || !parity || size == 0 || size >= (1ull << 31) || nobj == 0) return false;
+  const uint64_t bs = ((size + kK * 8 - 1) / (kK * 8) + 15) / 16 * 16 * 8;
+  if (stride < size || pstride < kR * bs || (stride & 15u) || (pstride & 15u) ||
+      ((uintptr_t)objs & 15u) || ((uintptr_t)parity & 15u))
+    return false;
+  *a = XorArgs{objs, stride, parity, pstride, (uint32_t)size, (uint32_t)bs,
+               (uint32_t)((bs + kLanes * 16 - 1) / (kLanes * 16))};
+  const uint64_t g = nobj * a->tiles;
+  if (g > 0x7FFFFFFFull) return false;
+  *grid = (uint32_t)g;
+  return true;
+}
+
 }  // namespace
 
 // Returns 0 on success, -1 on bad arguments, -2 on a launch error.
 extern "C" __attribute__((visibility("default"))) int leoec_measure_xor_pattern_dev(
     const uint8_t* objs, uint64_t stride, uint64_t size, uint64_t nobj, uint8_t* parity,
     uint64_t pstride, hipStream_t stream) {
-  if (!objs || !parity || size == 0 || size >= (1ull << 31) || nobj == 0) return -1;
-  const uint64_t bs = ((size + kK * 8 - 1) / (kK * 8) + 15) / 16 * 16 * 8;
-  if (stride < size || pstride < kR * bs || (stride & 15u) || (pstride & 15u) ||
-      ((uintptr_t)objs & 15u) || ((uintptr_t)parity & 15u))
+  XorArgs a;
+  uint32_t grid;
+  if (!xor_args(objs, stride, size, nobj, parity, pstride, &a, &grid)) return -1;
+  hipLaunchKernelGGL(xor_pattern, dim3(grid), dim3(kLanes), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// half = 0: the reads of xor_pattern alone (parity untouched); 1: its writes
+// alone (parity block r, lane l of a 16-byte column at byte `off` of object
+// o: the dwords {l % 64, o, off, r}).  Returns as above.
+extern "C" __attribute__((visibility("default"))) int leoec_measure_stream_half_dev(
+    int half, const uint8_t* objs, uint64_t stride, uint64_t size, uint64_t nobj, uint8_t* parity,
+    uint64_t pstride, hipStream_t stream) {
+  XorArgs a;
+  uint32_t grid;
+  if ((half != 0 && half != 1) || !xor_args(objs, stride, size, nobj, parity, pstride, &a, &grid))
     return -1;
-  XorArgs a{objs, stride, parity, pstride, (uint32_t)size, (uint32_t)bs,
-            (uint32_t)((bs + kLanes * 16 - 1) / (kLanes * 16))};
-  const uint64_t grid = nobj * a.tiles;
-  if (grid > 0x7FFFFFFFull) return -1;
-  hipLaunchKernelGGL(xor_pattern, dim3((uint32_t)grid), dim3(kLanes), 0, stream, a);
+  if (half == 0)
+    hipLaunchKernelGGL(stream_half<true>, dim3(grid), dim3(kLanes), 0, stream, a, 0x9E3779B9u);
+  else
+    hipLaunchKernelGGL(stream_half<false>, dim3(grid), dim3(kLanes), 0, stream, a, 0u);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

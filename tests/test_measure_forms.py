@@ -500,3 +500,49 @@ def test_host_batching_mixed_callers(gpu, le, oracle, form, measure):
         assert sum(1 for x in lanes[:4] if x > 0) >= (4 if "always" in form else 2), \
             list(lanes[:4])
         assert sum(lanes[4:]) == 0
+
+
+def test_pattern_kernels_do_what_they_claim(gpu, le):
+    """bench.py's pattern-ceiling kernels (measurement library,
+    csrc/xor_pattern.hip) on a ragged batch: xor_pattern writes every parity
+    block as the XOR of the 10 data blocks (zero past the object); the
+    read half writes nothing; the write half writes its documented pattern
+    and reads nothing."""
+    import ctypes
+
+    import torch
+
+    from leo_erasure_amd import _lib
+    mlib = _lib.measure_library()
+    n, size = 12, 300007
+    bs = ((size + 79) // 80 + 15) // 16 * 16 * 8
+    stride = (size + 15) // 16 * 16 + 64
+    g = torch.Generator(device="cuda").manual_seed(7)
+    objs = torch.randint(0, 256, (n, stride), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.full((n, 4 * bs), 0xAB, dtype=torch.uint8, device="cuda")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    args = (objs.data_ptr(), stride, size, n, parity.data_ptr(), 4 * bs, st)
+
+    assert mlib.leoec_measure_stream_half_dev(0, *args) == 0
+    torch.cuda.synchronize()
+    assert bool((parity == 0xAB).all()), "the read half wrote"
+
+    assert mlib.leoec_measure_xor_pattern_dev(*args) == 0
+    torch.cuda.synchronize()
+    host = objs.cpu().numpy()
+    data = np.zeros((n, 10 * bs), dtype=np.uint8)
+    data[:, :size] = host[:, :size]
+    want = np.bitwise_xor.reduce(data.reshape(n, 10, bs), axis=1)
+    got = parity.cpu().numpy().reshape(n, 4, bs)
+    for r in range(4):
+        assert np.array_equal(got[:, r], want), f"xor_pattern parity block {r}"
+
+    assert mlib.leoec_measure_stream_half_dev(1, *args) == 0
+    torch.cuda.synchronize()
+    got = parity.cpu().numpy().reshape(n, 4, bs // 16, 4 * 4).view(np.uint32).reshape(n, 4, bs // 16, 4)
+    off = np.arange(bs // 16, dtype=np.uint32) * 16
+    for o in (0, 5, n - 1):
+        for r in range(4):
+            exp = np.stack([(off // 16) % 64, np.full_like(off, o), off, np.full_like(off, r)], axis=1)
+            assert np.array_equal(got[o, r], exp), f"write half object {o} block {r}"
+    assert mlib.leoec_measure_stream_half_dev(2, *args) == -1
