@@ -87,6 +87,7 @@ struct Slot {
   int reserved = 0, filled = 0, readers = 0;
   int status = LEOEC_OK;    // the batch's copies and event: fails every job
   Clock::time_point opened, done;
+  std::condition_variable cv_done;  // this batch's callers (Knobs::hostq_wake = 1)
 };
 
 struct Queue {
@@ -102,6 +103,8 @@ struct Queue {
   std::deque<Slot*> inflight;  // launch order
   Slot* last = nullptr;        // most recently launched
   int direct = 0;              // calls on their per-thread path (HostqTicket)
+  int free_waiters = 0;        // callers waiting on cv_free
+  int done_waiters = 0;        // callers waiting on cv_done (Knobs::hostq_wake = 0)
 };
 
 // Wait for `ev` without holding the queue lock: (Knobs::hostq_sync = 1) a
@@ -297,7 +300,8 @@ void completer_main(Queue* q) {
     if (q->last == s) q->last = nullptr;
     if (s->status == LEOEC_OK) s->status = rc;
     s->state = St::kDone;
-    q->cv_done.notify_all();
+    s->cv_done.notify_all();  // this batch's callers
+    if (q->done_waiters > 0) q->cv_done.notify_all();  // (round-4 form: every caller)
     q->cv_worker.notify_one();
   }
 }
@@ -518,7 +522,9 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
         break;
       }
     if (!f) {
+      ++q->free_waiters;
       q->cv_free.wait(lk);
+      --q->free_waiters;
       continue;
     }
     f->state = St::kOpen;
@@ -543,7 +549,10 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
   s->out_off.push_back(oo);
   ++s->reserved;
   ++s->readers;
-  q->cv_worker.notify_one();
+  // the worker waits for an open slot's FIRST reservation (or a closed
+  // slot, or room on the GPU, notified where they happen)
+  const bool wake = knobs().hostq_wake == 1;
+  if (!wake || s->reserved == 1) q->cv_worker.notify_one();
   lk.unlock();
 
   const bool gather = job.in.size() > 1;
@@ -558,7 +567,13 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
   if (overlap) overlap(arg);
   lk.lock();
   const Clock::time_point tw = Clock::now();
-  q->cv_done.wait(lk, [s] { return s->state == St::kDone; });
+  if (wake) {
+    s->cv_done.wait(lk, [s] { return s->state == St::kDone; });
+  } else {
+    ++q->done_waiters;
+    q->cv_done.wait(lk, [s] { return s->state == St::kDone; });
+    --q->done_waiters;
+  }
   stat_add(8, us_since(tw));
   const int status = s->status != LEOEC_OK ? s->status : s->job_rc[idx];
   lk.unlock();
@@ -568,7 +583,7 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
   if (--s->readers == 0) {
     stat_add(7, us_since(s->done));
     s->state = St::kFree;
-    q->cv_free.notify_all();
+    if (q->free_waiters > 0) q->cv_free.notify_all();
   }
   return status;
 }

@@ -77,6 +77,7 @@ const Knobs* read_env() {
   k->hostq_zc = env_int("LEOEC_HOSTQ_ZC", k->hostq_zc);
   k->hostq_ntcopy = env_int("LEOEC_HOSTQ_NTCOPY", k->hostq_ntcopy);
   k->hostq_survivors = env_int("LEOEC_HOSTQ_SURVIVORS", k->hostq_survivors);
+  k->hostq_wake = env_int("LEOEC_HOSTQ_WAKE", k->hostq_wake);
   k->hostq_fail_bs = env_int("LEOEC_HOSTQ_FAIL_BS", k->hostq_fail_bs);
   k->gf8_variant = env_int("LEOEC_GF8_VARIANT", k->gf8_variant);
   k->gf8_tmap = env_int("LEOEC_GF8_TMAP", k->gf8_tmap);

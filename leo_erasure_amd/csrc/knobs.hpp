@@ -47,6 +47,10 @@ struct Knobs {
   int hostq_ntcopy = 1;      // LEOEC_HOSTQ_NTCOPY=0: callers pack gathered inputs (decode /
                              //   repair) into the pinned buffers with memcpy instead of
                              //   non-temporal stores (host_copy.hpp; shipped since round 4)
+  int hostq_wake = 1;        // LEOEC_HOSTQ_WAKE: 1 targeted wake-ups (a batch's callers on
+                             //   its slot's condition variable; the worker woken by a
+                             //   slot's first reservation only; slot-free waiters counted),
+                             //   0 the round-4 broadcasts (every waiting caller per batch)
   int hostq_survivors = 1;   // LEOEC_HOSTQ_SURVIVORS: where a batched decode copies its
                              //   surviving data blocks into the output: 1 while its batch
                              //   is on the GPU, 0 before joining the batch, 2 after its

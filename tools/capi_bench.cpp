@@ -14,6 +14,8 @@
 //                                                        decode from 1, 8, 32 threads
 //   tools/capi_bench <libleoec*.so> threads  [K=V,...]   first calls of new threads
 //                                                        after gf_init on the main one
+//   tools/capi_bench <libleoec*.so> sizes    [K=V,...]   callers() at 16 KiB - 4 MiB
+//                                                        objects, 8 and 32 threads
 // K=V: measurement-build knobs (leoec_measure_set_knob), applied after load.
 #include <dlfcn.h>
 
@@ -38,7 +40,10 @@ using Decode = int (*)(int, int, int, int, const uint8_t* const*, const int*, in
                        uint64_t, uint8_t*);
 using SetKnob = int (*)(const char*, const char*);
 
+using Stats = void (*)(double*);
+
 GfInit gf_init;
+Stats hostq_stats;  // measurement build only (nullptr otherwise)
 Layout layout;
 Encode encode;
 Decode decode;
@@ -105,11 +110,11 @@ void ref_bench(int reps) {
   }
 }
 
-// tools/e2e_bench.py's callers(): T threads calling back to back, 1 MiB
-// RS(10,4,8) objects, 3 trials of 0.4 s after a warm-up trial, median.
-void callers(int T, bool dec) {
+// tools/e2e_bench.py's callers(): T threads calling back to back, RS(10,4,8)
+// objects of `size` bytes (1 MiB: the bench's), 3 trials of 0.4 s after a
+// warm-up trial, median.
+void callers(int T, bool dec, uint64_t size = 1ull << 20) {
   const int K = 10, M = 4, W = 8;
-  const uint64_t size = 1ull << 20;
   uint64_t bs;
   int filled;
   if (layout(2, K, M, W, size, &bs, &filled)) exit(3);
@@ -130,6 +135,7 @@ void callers(int T, bool dec) {
                                    : outs[t].data() + (uint64_t)(i - filled) * bs);
   }
   std::atomic<int> errs{0};
+  double calls_per_s = 0;
   auto call = [&](int t) {
     const int rc = dec ? decode(2, K, M, W, ptrs[t].data(), ids.data(), (int)ids.size(), bs, size,
                                 decs[t].data())
@@ -162,10 +168,14 @@ void callers(int T, bool dec) {
     const double dt = now_s() - t0;
     long n = 0;
     for (long c : counts) n += c;
+    calls_per_s = n / dt;
     return n * (double)size / dt / (double)(1ull << 30);
   };
   trial(0.4);
+  double st[14] = {};
+  if (hostq_stats) hostq_stats(st);  // reset
   std::vector<double> r = {trial(0.4), trial(0.4), trial(0.4)};
+  if (hostq_stats) hostq_stats(st);
   std::sort(r.begin(), r.end());
   if (dec)
     for (int t = 0; t < T; ++t)
@@ -173,9 +183,26 @@ void callers(int T, bool dec) {
         fprintf(stderr, "decode mismatch\n");
         exit(6);
       }
-  printf("{\"path\": \"C ABI leoec_%s, 1 MiB objects, %d caller threads, system HIP runtime\", "
-         "\"GiBps\": %.2f, \"GiBps_min_max\": [%.2f, %.2f], \"errors\": %d}\n",
-         dec ? "decode" : "encode", T, r[1], r[0], r[2], errs.load());
+  std::string q;
+  if (hostq_stats && st[0] > 0) {
+    // per batch: jobs, then the timeline (us): worker waiting for fills,
+    // issue, completer waiting on the GPU, open -> close, done -> free;
+    // per job: caller waiting for DONE, waiting to reserve
+    char b[512];
+    snprintf(b, sizeof b,
+             ", \"queue\": {\"batches\": %.0f, \"jobs_per_batch\": %.2f, \"launches_per_batch\": %.2f, "
+             "\"fill_wait_us\": %.1f, \"issue_us\": %.1f, \"gpu_wait_us\": %.1f, "
+             "\"open_to_close_us\": %.1f, \"done_to_free_us\": %.1f, \"caller_wait_us_per_job\": %.1f, "
+             "\"reserve_wait_us_per_job\": %.1f}",
+             st[0], st[1] / st[0], st[2] / st[0], st[3] / st[0], st[4] / st[0], st[5] / st[0],
+             st[6] / st[0], st[7] / st[0], st[8] / std::max(st[1], 1.0), st[9] / std::max(st[1], 1.0));
+    q = b;
+  }
+  printf("{\"path\": \"C ABI leoec_%s, %llu B objects, %d caller threads, system HIP runtime\", "
+         "\"GiBps\": %.2f, \"GiBps_min_max\": [%.2f, %.2f], \"calls_per_s_last_trial\": %.0f, "
+         "\"errors\": %d%s}\n",
+         dec ? "decode" : "encode", (unsigned long long)size, T, r[1], r[0], r[2], calls_per_s,
+         errs.load(), q.c_str());
   fflush(stdout);
 }
 
@@ -261,6 +288,7 @@ int main(int argc, char** argv) {
   layout = (Layout)sym(h, "leoec_layout");
   encode = (Encode)sym(h, "leoec_encode");
   decode = (Decode)sym(h, "leoec_decode");
+  hostq_stats = (Stats)dlsym(h, "leoec_measure_hostq_stats");
   if (argc > 3 && argv[3][0]) {
     auto set = (SetKnob)sym(h, "leoec_measure_set_knob");
     std::string kv = argv[3];
@@ -289,6 +317,16 @@ int main(int argc, char** argv) {
     new_threads();
   } else if (mode == "lone") {
     lone(2000);
+  } else if (mode == "small") {
+    // 16 KiB objects, 32 callers, encode (the queue's per-call cost)
+    callers(32, false, 16ull << 10);
+    callers(32, false, 64ull << 10);
+  } else if (mode == "sizes") {
+    // objects from 16 KiB to 4 MiB: the host path's per-call cost against
+    // its bytes (RS(10,4,8); 8 and 32 callers)
+    for (uint64_t size : {16ull << 10, 64ull << 10, 256ull << 10, 1ull << 20, 4ull << 20})
+      for (bool dec : {false, true})
+        for (int T : {8, 32}) callers(T, dec, size);
   } else {
     for (bool dec : {false, true})
       for (int T : {1, 8, 32}) callers(T, dec);
