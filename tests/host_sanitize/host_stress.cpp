@@ -195,6 +195,8 @@ int main(int argc, char** argv) {
         leoec_measure_set_knob("LEOEC_HOSTQ_NTCOPY", (i / 3) % 2 ? "1" : "0");
         leoec_measure_set_knob("LEOEC_HOSTQ_SURVIVORS", i % 3 == 0 ? "0" : i % 3 == 1 ? "1" : "2");
         leoec_measure_set_knob("LEOEC_ZC_CHUNKS", i % 4 == 0 ? "1" : i % 4 == 1 ? "2" : i % 4 == 2 ? "3" : "8");
+        // targeted / broadcast wake-ups, flipped while callers wait in both forms
+        leoec_measure_set_knob("LEOEC_HOSTQ_WAKE", (i / 5) % 2 ? "0" : "1");
         ++i;
         std::this_thread::sleep_for(std::chrono::milliseconds(3));
       }
