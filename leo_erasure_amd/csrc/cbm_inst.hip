@@ -255,6 +255,14 @@ bool launch_cbm(const GfBitApply& p, hipStream_t s, int* rc) {
     case 3: *rc = launch_cbm_t<Cbm10_4, 128, 2, 16>(p, s); return true;
     case 4: *rc = launch_cbm_t<Cbm10_4, 64, 3, 4>(p, s); return true;
     case 5: *rc = launch_cbm_t<Cbm10_4, 256, 2, 16>(p, s); return true;
+    // round 6: one wave per SIMD (up to 512 VGPRs) with deep look-ahead, the
+    // register regime of the 16-byte-lane XOR pattern that read 0.77
+    // (tools/packet_ceiling.hip pattern<4,128>: 276 VGPRs, every load of a
+    // block pair in flight)
+    case 6: *rc = launch_cbm_t<Cbm10_4, 128, 1, 32>(p, s); return true;
+    case 7: *rc = launch_cbm_t<Cbm10_4, 64, 1, 32>(p, s); return true;
+    case 8: *rc = launch_cbm_t<Cbm10_4, 128, 1, 48>(p, s); return true;
+    case 9: *rc = launch_cbm_t<Cbm10_4, 256, 1, 32>(p, s); return true;
     default: *rc = launch_cbm_t<Cbm10_4, 64, 2, 16>(p, s); return true;
   }
 }

@@ -223,7 +223,7 @@ def test_xcd_object_map_batches(gpu, le, oracle, measure, cls, k, m, w):
         assert outs[0][o, :m * bs].tobytes() == b"".join(r[k:]), f"object {o}"
 
 
-@pytest.mark.parametrize("form", ["1", "2", "3", "4", "5"])
+@pytest.mark.parametrize("form", ["1", "2", "3", "4", "5", "6", "7", "8", "9"])
 def test_cauchy_compiled_bitmatrix_batches(gpu, le, oracle, measure, form):
     """cauchyrs(10,4,8) encode with its bitmatrix compiled in (cbm_inst.hip,
     LEOEC_GFBIT_CBM): batches of whole and ragged 1 MiB objects (a short last
@@ -250,13 +250,18 @@ def test_cauchy_compiled_bitmatrix_batches(gpu, le, oracle, measure, form):
 
 @pytest.mark.parametrize("form,env", [
     ("3", {}), ("3", {"LEOEC_GFBIT_WG": "256"}), ("3", {"LEOEC_GFBIT_PF": "2"}),
-    ("3", {"LEOEC_GFBIT_PF": "3"}), ("3", {"LEOEC_GFBIT_PF": "4"}), ("3", {"LEOEC_GFBIT_PF": "5"})],
+    ("3", {"LEOEC_GFBIT_PF": "3"}), ("3", {"LEOEC_GFBIT_PF": "4"}), ("3", {"LEOEC_GFBIT_PF": "5"}),
+    ("5", {}), ("5", {"LEOEC_GFBIT_PF": "2"}), ("5", {"LEOEC_GFBIT_PF": "3"}),
+    ("5", {"LEOEC_GFBIT_WG": "64"}), ("5", {"LEOEC_GFBIT_WG": "64", "LEOEC_GFBIT_PF": "3"}),
+    ("5", {"LEOEC_GFBIT_WG": "256"}), ("5", {"LEOEC_GFBIT_WAVES": "2", "LEOEC_GFBIT_PF": "2"})],
     ids=lambda e: e if isinstance(e, str) else (",".join(f"{k}={v}" for k, v in e.items()) or "default"))
 def test_cauchy_16B_forms_batches(gpu, le, oracle, measure, form, env):
-    """cauchyrs through the 16-byte-access form gfba_apply
+    """cauchyrs through the 16-byte-access forms gfba_apply
     (LEOEC_GFBIT_FORM=3: line-aligned 16-byte copies into per-wave LDS slots,
     read back at each packet's phase; round 4's gfbs_apply, form 4, ran here
-    too before it was removed, code at cd96abc).  Object rows at every
+    too before it was removed, code at cd96abc) and gfbk_apply (FORM=5: K = 10
+    compiled in, 16-byte lanes, one wave per SIMD, blocks of loads in flight;
+    the other k fall back to the shipped kernel).  Object rows at every
     16-byte phase mod 128 (row stride = k*bs + 48), sizes whose blocks are
     full, short (last block 103,936 of 104,960 B), one packet of 16 B, and
     empty (size 1,040: block 9 holds nothing); encode parity equal to the
