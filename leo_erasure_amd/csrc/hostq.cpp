@@ -1,10 +1,14 @@
 // hostq.cpp — see hostq.hpp.
 //
 // Per device: kSlots batch slots, each a pinned input arena + pinned output
-// arena + their device twins, a stream and an event.  A slot moves
+// arena + their device twins, a stream and its events, and two copy streams
+// shared by the slots (every batch's H2D on one, every D2H on the other: the
+// link's two directions overlap only when their copies are on separate
+// streams, tools/duplex_probe.hip).  A slot moves
 //   FREE -> OPEN (callers reserve space and copy their inputs in)
 //        -> CLOSED (no more reservations; the worker waits for the copies)
-//        -> INFLIGHT (H2D, launches, D2H enqueued on the slot's stream)
+//        -> INFLIGHT (H2D on the input-copy stream, launches on the slot's
+//                     stream, D2H on the output-copy stream, chained by events)
 //        -> DONE (callers copy their outputs out) -> FREE (last reader).
 // The worker closes the open slot whenever fewer than Knobs::hostq_depth
 // batches are on the GPU, so calls arriving while the GPU is busy pile into
@@ -74,11 +78,14 @@ struct Slot {
   uint8_t* d_out = nullptr;
   uint8_t* z_in = nullptr;   // device addresses of h_in / h_out (zero-copy batches)
   uint8_t* z_out = nullptr;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // the slot's launches
+  hipStream_t up = nullptr;      // the queue's input-copy stream (every slot's H2D)
+  hipStream_t down = nullptr;    // the queue's output-copy stream (every slot's D2H)
   hipEvent_t ev = nullptr;
   hipEvent_t ev_blk = nullptr;  // the same, created hipEventBlockingSync (Knobs::hostq_sync = 2)
   hipEvent_t ev_done = nullptr; // the one recorded for this batch (ev or ev_blk)
   hipEvent_t ev_h2d = nullptr;  // after the input copy: the H2D engine is free for the next batch
+  hipEvent_t ev_k = nullptr;    // after the launches: the output copy may start
   uint64_t used_in = 0, used_out = 0;
   std::vector<const HostJob*> jobs;
   std::vector<uint64_t> in_off, out_off;
@@ -92,6 +99,7 @@ struct Slot {
 
 struct Queue {
   int device = -1;
+  hipStream_t up = nullptr, down = nullptr;  // the copy streams (Slot::up / down)
   std::mutex mu;
   std::condition_variable cv_worker;    // work for the worker (jobs, fills, GPU room)
   std::condition_variable cv_complete;  // work for the completer
@@ -132,7 +140,8 @@ int slot_alloc(Slot* s) {
       hipEventCreateWithFlags(&s->ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&s->ev_blk, hipEventDisableTiming | hipEventBlockingSync) !=
           hipSuccess ||
-      hipEventCreateWithFlags(&s->ev_h2d, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&s->ev_h2d, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_k, hipEventDisableTiming) != hipSuccess) {
     if (s->h_in) (void)hipHostFree(s->h_in);
     if (s->h_out) (void)hipHostFree(s->h_out);
     if (s->d_in) (void)hipFree(s->d_in);
@@ -158,6 +167,12 @@ bool same_map(const HostJob& a, const HostJob& b) {
 // Enqueue one batch: ONE H2D of the input arena, one launch per run of
 // consecutive identical maps (their regions are uniformly strided: they were
 // reserved back to back with the same sizes), ONE D2H of the output arena.
+// The copies go on the queue's two copy streams (Knobs::hostq_streams = 1,
+// shipped), the launches on the slot's stream after the H2D's event, the
+// D2H after the launches' event: batch b's D2H then runs beside batch b+1's
+// H2D on the full-duplex link.  (hostq_streams = 0: all three on the slot's
+// stream, the round-2..5 form, whose copies of neighbouring batches did not
+// overlap on the link: profiles/r05_s19_duplex_queue.log.)
 // Plans were built by the callers, so a launch can fail only for its own
 // jobs (s->job_rc); the other runs are still launched.  The event is
 // recorded whatever happened, so the completer always waits for the work
@@ -170,12 +185,17 @@ int launch_slot(Slot* s) {
   const bool zc = knobs().hostq_zc != 0;
   uint8_t* din = zc ? s->z_in : s->d_in;
   uint8_t* dout = zc ? s->z_out : s->d_out;
+  const bool split = !zc && knobs().hostq_streams == 1 && s->up && s->down;
+  hipStream_t cin = split ? s->up : s->stream;     // the input copy's stream
+  hipStream_t cout = split ? s->down : s->stream;  // the output copy's stream
   int rc = zc ? LEOEC_OK
-              : hipMemcpyAsync(s->d_in, s->h_in, s->used_in, hipMemcpyHostToDevice, s->stream) ==
+              : hipMemcpyAsync(s->d_in, s->h_in, s->used_in, hipMemcpyHostToDevice, cin) ==
                         hipSuccess
                     ? LEOEC_OK
                     : LEOEC_E_HIP;
-  if (rc == LEOEC_OK && !zc && hipEventRecord(s->ev_h2d, s->stream) != hipSuccess) rc = LEOEC_E_HIP;
+  if (rc == LEOEC_OK && !zc && hipEventRecord(s->ev_h2d, cin) != hipSuccess) rc = LEOEC_E_HIP;
+  if (rc == LEOEC_OK && split && hipStreamWaitEvent(s->stream, s->ev_h2d, 0) != hipSuccess)
+    rc = LEOEC_E_HIP;
   stat_add(11, us_since(t));
   t = Clock::now();
   const size_t n = s->jobs.size();
@@ -209,14 +229,27 @@ int launch_slot(Slot* s) {
   t = Clock::now();
   if (rc == LEOEC_OK && zc && hipEventRecord(s->ev_h2d, s->stream) != hipSuccess)
     rc = LEOEC_E_HIP;  // (zero-copy: the inputs are consumed when the launches end)
+  if (rc == LEOEC_OK && split &&
+      (hipEventRecord(s->ev_k, s->stream) != hipSuccess ||
+       hipStreamWaitEvent(cout, s->ev_k, 0) != hipSuccess))
+    rc = LEOEC_E_HIP;
   if (rc == LEOEC_OK && !zc &&
-      hipMemcpyAsync(s->h_out, s->d_out, s->used_out, hipMemcpyDeviceToHost, s->stream) !=
-          hipSuccess)
+      hipMemcpyAsync(s->h_out, s->d_out, s->used_out, hipMemcpyDeviceToHost, cout) != hipSuccess)
     rc = LEOEC_E_HIP;
   stat_add(13, us_since(t));
   s->ev_done = knobs().hostq_sync == 2 ? s->ev_blk : s->ev;
-  if (hipEventRecord(s->ev_done, s->stream) != hipSuccess) {
-    (void)hipStreamSynchronize(s->stream);  // no event to wait on: drain here
+  hipStream_t last = cout;
+  if (split && rc != LEOEC_OK) {
+    // a failure part-way: drain whatever this batch enqueued on the three
+    // streams, so the event below (on the slot's stream) follows all of it
+    (void)hipStreamSynchronize(cin);
+    (void)hipStreamSynchronize(s->stream);
+    (void)hipStreamSynchronize(cout);
+    last = s->stream;
+  }
+  if (hipEventRecord(s->ev_done, last) != hipSuccess) {
+    (void)hipStreamSynchronize(last);  // no event to wait on: drain here
+    if (split) (void)hipStreamSynchronize(s->stream);
     if (rc == LEOEC_OK) rc = LEOEC_E_HIP;
   }
   return rc;
@@ -390,13 +423,20 @@ Queue* build_queue(int lane) {
   if (!on.ok()) return nullptr;
   Queue* q = new Queue;
   q->device = dev;
+  if (hipStreamCreateWithFlags(&q->up, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&q->down, hipStreamNonBlocking) != hipSuccess)
+    return nullptr;
   for (Slot& sl : q->slots) {
     sl.lane = lane;
+    sl.up = q->up;
+    sl.down = q->down;
+    // each arena's first copy on the stream it will use (and the slot's own)
     if (slot_alloc(&sl) != LEOEC_OK ||
-        hipMemcpyAsync(sl.d_in, sl.h_in, kSlotBytes, hipMemcpyHostToDevice, sl.stream) !=
+        hipMemcpyAsync(sl.d_in, sl.h_in, kSlotBytes, hipMemcpyHostToDevice, q->up) != hipSuccess ||
+        hipMemcpyAsync(sl.h_out, sl.d_out, kSlotBytes, hipMemcpyDeviceToHost, q->down) !=
             hipSuccess ||
-        hipMemcpyAsync(sl.h_out, sl.d_out, kSlotBytes, hipMemcpyDeviceToHost, sl.stream) !=
-            hipSuccess ||
+        hipStreamSynchronize(q->up) != hipSuccess || hipStreamSynchronize(q->down) != hipSuccess ||
+        hipMemcpyAsync(sl.d_out, sl.h_out, 4096, hipMemcpyHostToDevice, sl.stream) != hipSuccess ||
         hipStreamSynchronize(sl.stream) != hipSuccess)
       return nullptr;
   }

@@ -68,8 +68,9 @@ const Knobs* read_env() {
   k->host_batch = env_int("LEOEC_HOST_BATCH", k->host_batch);
   k->batch_window_us = env_int("LEOEC_BATCH_WINDOW_US", k->batch_window_us);
   k->hostq_depth = env_int("LEOEC_HOSTQ_DEPTH", k->hostq_depth);
-  if (k->hostq_depth < 1 || k->hostq_depth > 3) k->hostq_depth = 3;
+  if (k->hostq_depth < 1 || k->hostq_depth > 4) k->hostq_depth = 3;  // 5 slots: one stays open
   k->hostq_sync = env_int("LEOEC_HOSTQ_SYNC", k->hostq_sync);
+  k->hostq_streams = env_int("LEOEC_HOSTQ_STREAMS", k->hostq_streams);
   k->hostq_close = env_int("LEOEC_HOSTQ_CLOSE", k->hostq_close);
   k->hostq_direct = env_int("LEOEC_HOSTQ_DIRECT", k->hostq_direct);
   k->hostq_direct_map = env_int("LEOEC_HOSTQ_DIRECT_MAP", k->hostq_direct_map);

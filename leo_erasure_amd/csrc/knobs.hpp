@@ -30,6 +30,8 @@ struct Knobs {
   int host_batch = 1;        // LEOEC_HOST_BATCH=0: host calls take the per-thread path only
   int batch_window_us = 0;   // LEOEC_BATCH_WINDOW_US: hold an idle-GPU batch open this long
   int hostq_depth = 3;       // LEOEC_HOSTQ_DEPTH: batches on the GPU at once
+  int hostq_streams = 1;     // LEOEC_HOSTQ_STREAMS: 1 a batch's H2D / D2H on the queue's two copy
+                             // streams (shipped), 0 everything on the slot's stream
   int hostq_sync = 1;        // LEOEC_HOSTQ_SYNC: 1 poll events (hipEventQuery + yield),
                              //   0 hipEventSynchronize, 2 the same on blocking-sync events
   int hostq_close = 1;       // LEOEC_HOSTQ_CLOSE: 1 close a batch when the previous H2D is

@@ -359,5 +359,20 @@ inline hipError_t hipEventSynchronize(hipEvent_t e) {
   return hipSuccess;
 }
 
+// Later work on s waits for what preceded e's record (on e's stream): the
+// wait is an operation of s's own thread, as the device's barrier packet.
+inline hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned) {
+  fakehip::Stream* on;
+  uint64_t t;
+  {
+    std::lock_guard<std::mutex> l(e->mu);
+    on = e->s;
+    t = e->t;
+  }
+  if (!on) return hipSuccess;  // never recorded: nothing to wait for
+  fake_stream(s)->push([on, t] { on->wait(t); });
+  return hipSuccess;
+}
+
 inline const char* hipGetErrorString(hipError_t) { return "fake hip error"; }
 inline hipError_t hipGetLastError() { return hipSuccess; }

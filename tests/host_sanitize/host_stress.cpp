@@ -197,6 +197,7 @@ int main(int argc, char** argv) {
         leoec_measure_set_knob("LEOEC_ZC_CHUNKS", i % 4 == 0 ? "1" : i % 4 == 1 ? "2" : i % 4 == 2 ? "3" : "8");
         // targeted / broadcast wake-ups, flipped while callers wait in both forms
         leoec_measure_set_knob("LEOEC_HOSTQ_WAKE", (i / 5) % 2 ? "0" : "1");
+        leoec_measure_set_knob("LEOEC_HOSTQ_STREAMS", (i / 7) % 2 ? "0" : "1");
         ++i;
         std::this_thread::sleep_for(std::chrono::milliseconds(3));
       }
