@@ -397,7 +397,10 @@ class GpuBackend:
         out = {"h2d_GBps": round(timed(True, False), 1), "d2h_GBps": round(timed(False, True), 1),
                "both_GBps": round(timed(True, True), 1),
                "what": f"pinned {mib} MiB copies, median of {reps}; both = the two directions "
-                       "at once on two streams, bytes of both / time"}
+                       "at once on two streams, bytes of both / time, on this process's HIP "
+                       "runtime (the torch wheel's, whose two copies do not overlap; the system "
+                       "runtime a NIF loads moves both at once at ~97 GB/s: DESIGN.md "
+                       "End-to-end)"}
         del hsrc, hdst, dsrc, ddst
         return out
 
