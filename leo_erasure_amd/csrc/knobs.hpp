@@ -36,10 +36,13 @@ struct Knobs {
                              //   0 hipEventSynchronize, 2 the same on blocking-sync events
   int hostq_close = 1;       // LEOEC_HOSTQ_CLOSE: 1 close a batch when the previous H2D is
                              //   done, 0 as soon as the GPU has room
-  int hostq_direct = 4;      // LEOEC_HOSTQ_DIRECT: encode calls that may take the per-thread
+  int hostq_direct = 16;     // LEOEC_HOSTQ_DIRECT: encode calls that may take the per-thread
                              //   path while the queue is idle (0: every call batched)
-  int hostq_direct_map = 2;  // LEOEC_HOSTQ_DIRECT_MAP: the same for decode / repair (their
+  int hostq_direct_map = 8;  // LEOEC_HOSTQ_DIRECT_MAP: the same for decode / repair (their
                              //   per-thread path gathers k buffers: it tops out sooner)
+                             //   (round 5: 16 / 8, was 4 / 2: encode +21 % at 8 callers,
+                             //   +17 % at 16, decode +30 % at 4, +27 % at 8, 32 callers
+                             //   unchanged; profiles/r05_s26_*.log, three rotated rounds)
   int hostq_fail_bs = 0;     // LEOEC_HOSTQ_FAIL_BS: batched launches of this block size report
                              //   a HIP error (fault injection: per-job status)
   int hostq_zc = 0;          // LEOEC_HOSTQ_ZC=1: batches without DMA copies (kernels on the

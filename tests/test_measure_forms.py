@@ -457,7 +457,8 @@ def test_host_pinned_large_objects(gpu, le, oracle, pin_kib, measure):
 
 
 @pytest.mark.parametrize("form", ["always-batch", "per-thread", "lanes4",
-                                  "lanes4-always-batch", "fail-one", "zc-batch"])
+                                  "lanes4-always-batch", "fail-one", "zc-batch",
+                                  "always-batch-slot-stream", "fail-one-slot-stream"])
 def test_host_batching_mixed_callers(gpu, le, oracle, form, measure):
     """gpu_helpers.mixed_callers under the measurement build's queue
     policies: every call through the queue (always-batch) or none
@@ -467,9 +468,14 @@ def test_host_batching_mixed_callers(gpu, le, oracle, form, measure):
     makes the batched launches of one spec (cauchyrs(4,2,3) on 5000 B, bs
     1296) report a HIP error: its encodes, repairs and data-rebuilding
     decodes fail with LEOEC_E_HIP, every other call of the same batches
-    succeeds bit-exact."""
+    succeeds bit-exact.  The queue's copies run on its two copy streams
+    (shipped) except in the "-slot-stream" forms (LEOEC_HOSTQ_STREAMS=0: a
+    batch's copies and launches all on its slot's stream)."""
     import ctypes
     fail_bs = None
+    if form.endswith("-slot-stream"):
+        measure.setenv("LEOEC_HOSTQ_STREAMS", "0")
+        form = form[:-len("-slot-stream")]
     if form in ("always-batch", "lanes4-always-batch", "fail-one", "zc-batch"):
         measure.setenv("LEOEC_HOSTQ_DIRECT", "0")
         measure.setenv("LEOEC_HOSTQ_DIRECT_MAP", "0")

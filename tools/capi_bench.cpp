@@ -14,6 +14,8 @@
 //                                                        decode from 1, 8, 32 threads
 //   tools/capi_bench <libleoec*.so> threads  [K=V,...]   first calls of new threads
 //                                                        after gf_init on the main one
+//   tools/capi_bench <libleoec*.so> few      [K=V,...]   callers() from 1, 2, 4, 8 threads
+//   tools/capi_bench <libleoec*.so> mid      [K=V,...]   callers() from 4, 8, 16, 32 threads
 //   tools/capi_bench <libleoec*.so> sizes    [K=V,...]   callers() at 16 KiB - 4 MiB
 //                                                        objects, 8 and 32 threads
 // K=V: measurement-build knobs (leoec_measure_set_knob), applied after load.
@@ -317,6 +319,15 @@ int main(int argc, char** argv) {
     new_threads();
   } else if (mode == "lone") {
     lone(2000);
+  } else if (mode == "few") {
+    // the reference's basho_bench concurrency (test/basho_bench_leo_erasure_
+    // rs_10_4_8_1M_w_t1 / _t4.config: {concurrent, 1 | 4}) and 2
+    for (bool dec : {false, true})
+      for (int T : {1, 2, 4, 8}) callers(T, dec);
+  } else if (mode == "mid") {
+    // where the per-thread path hands over to the batching queue
+    for (bool dec : {false, true})
+      for (int T : {4, 8, 16, 32}) callers(T, dec);
   } else if (mode == "small") {
     // 16 KiB objects, 32 callers, encode (the queue's per-call cost)
     callers(32, false, 16ull << 10);
