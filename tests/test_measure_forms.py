@@ -484,6 +484,9 @@ def test_host_batching_mixed_callers(gpu, le, oracle, form, measure):
     if form.startswith("lanes4"):
         measure.setenv("LEOEC_HOSTQ_LANES", "4")
         assert len(le._lib.host_lanes()) == 4
+        if form == "lanes4":  # some calls per-thread, enough batched to reach every lane
+            measure.setenv("LEOEC_HOSTQ_DIRECT", "4")
+            measure.setenv("LEOEC_HOSTQ_DIRECT_MAP", "2")
     if form == "zc-batch":
         measure.setenv("LEOEC_HOSTQ_ZC", "1")
     if form == "fail-one":
