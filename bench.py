@@ -87,6 +87,8 @@ def parse(argv=None):
                    help="timed seconds per op of the host-memory leg")
     # internal: the pattern-ceiling child process (GpuBackend.pattern_ceiling_child)
     p.add_argument("--pattern-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--host-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--host-data", default="", help=argparse.SUPPRESS)
     p.add_argument("--pattern-device", type=int, default=0, help=argparse.SUPPRESS)
     p.add_argument("--pattern-seed", type=int, default=0x1E0E, help=argparse.SUPPRESS)
     p.add_argument("--traffic", default=",".join(
@@ -255,119 +257,58 @@ class GpuBackend:
                     "error": f"pattern child rc {r.returncode}: {r.stderr.strip()[-400:]}"}
         return json.loads(lines[-1])
 
-    def host_path(self, objs, parity, size, bs, callers=32, seconds=1.0):
+    def host_path(self, objs, parity, size, bs, callers=32, seconds=1.0, timeout=240):
         """The NIF's path end to end (PCIe-inclusive; never the bench value):
-        host-memory leoec_encode / leoec_decode through the C ABI from
-        `callers` threads, each with one object of this rank's batch copied
-        to host memory, back to back for `seconds` per op, on this rank's
-        device (leoec_host_spread([device]): the threads' own current device
-        would be device 0).  Checked, outside the timed loops: every thread's
-        encode parity equals the GPU's device parity of its object, and every
-        decode (data blocks 0-3 lost) returns the object."""
-        import ctypes
-        import threading
+        `host_rates` in a child process that keeps torch out
+        (LEOEC_NO_TORCH=1), so libleoec.so binds the system HIP runtime, as
+        in an Erlang VM that loads the NIF — the torch wheel's bundled
+        runtime does not overlap the link's two directions (DESIGN.md
+        End-to-end).  The child gets this rank's first `callers` objects and
+        their GPU parity through files, and measures on this rank's device.
+        The same leg in this process (the torch runtime) stays beside it as
+        `torch_runtime`."""
+        import tempfile
 
         import numpy as np
-        le = self.le
-        L = le.lib
         n = min(callers, objs.shape[0])
-        srcs = [np.ascontiguousarray(r) for r in objs[:n, :size].cpu().numpy()]
-        gpar = parity[:n].cpu().numpy()
-        filled = min(size // bs, K)
-        out_bytes = (K + M - filled) * bs
-        outs = [np.empty(out_bytes, dtype=np.uint8) for _ in range(n)]
-        decs = [np.empty(size, dtype=np.uint8) for _ in range(n)]
-        ids = list(range(len(ERASED), K + M))  # survivors: blocks 4..13
-        idv = (ctypes.c_int * len(ids))(*ids)
-
-        def block(t, i):
-            if i < filled:
-                return srcs[t].ctypes.data + i * bs
-            return outs[t].ctypes.data + (i - filled) * bs
-
-        def enc(t):
-            return L.leoec_encode(2, K, M, W, srcs[t].ctypes.data, size, outs[t].ctypes.data,
-                                  out_bytes)
-
-        ptrs = []
-
-        def dec(t):
-            return L.leoec_decode(2, K, M, W, ptrs[t], idv, len(ids), bs, size,
-                                  decs[t].ctypes.data)
-
-        def check():
-            enc_ok = all(np.array_equal(outs[t][(K - filled) * bs:], gpar[t]) for t in range(n))
-            dec_ok = all(np.array_equal(decs[t], srcs[t]) for t in range(n))
-            return enc_ok, dec_ok
-
-        def timed(fn):
-            errs, counts, box = [], [0] * n, {}
-            ready = threading.Barrier(n + 1)
-            go = threading.Event()
-
-            def work(t):
-                if fn(t) != 0:  # this thread's first call, outside the clock
-                    errs.append(t)
-                ready.wait()
-                go.wait()
-                c = 0
-                while time.perf_counter() < box["end"]:
-                    if fn(t) != 0:
-                        errs.append(t)
-                    c += 1
-                counts[t] = c
-
-            ths = [threading.Thread(target=work, args=(t,)) for t in range(n)]
-            for th in ths:
-                th.start()
-            ready.wait()
-            t0 = time.perf_counter()
-            box["end"] = t0 + seconds
-            go.set()
-            for th in ths:
-                th.join()
-            dt = time.perf_counter() - t0
-            if errs:
-                raise RuntimeError(f"host-path calls failed on threads {sorted(set(errs))[:8]}")
-            return sum(counts) * size / dt / 2**30, sum(counts)
-
-        le._lib.host_spread([self.index])
-        try:
-            for t in range(n):
-                if enc(t) != 0:
-                    raise RuntimeError("leoec_encode failed")
-            ptrs[:] = [(ctypes.c_void_p * len(ids))(*[block(t, i) for i in ids]) for t in range(n)]
-            enc_gibs, enc_calls = timed(enc)
-            dec_gibs, dec_calls = timed(dec)
-            enc_ok, dec_ok = check()
-        finally:
-            le._lib.host_spread([])
-        link = self.link_rates()
-        # Bytes each op moves per payload byte: an encode its object host ->
-        # device and its m parity blocks back, a decode its K survivor blocks
-        # in and its rebuilt blocks back.  `link_busy` = the share of each
-        # second those bytes keep the link busy at the copy rates measured
-        # alone (H2D then D2H); near 1 means the op runs at the link.
-        e = len(ERASED)
-        per = {"encode": (1.0, M * bs / size), "decode": (K * bs / size, e * bs / size)}
-        rate = {"encode": enc_gibs, "decode": dec_gibs}
-        busy = {op: round(rate[op] * 2**30 / 1e9 * (h / link["h2d_GBps"] + d / link["d2h_GBps"]), 3)
-                for op, (h, d) in per.items()}
-        return {"encode_GiBps": round(enc_gibs, 2), "decode_GiBps": round(dec_gibs, 2),
-                "callers": n, "seconds_per_op": seconds, "calls": [enc_calls, dec_calls],
-                "link": link, "link_busy": busy,
-                "parity_vs_gpu": {"objects": n, "encode_equal": enc_ok, "decode_equal": dec_ok},
-                "what": f"C ABI leoec_encode / leoec_decode (data blocks {ERASED} lost) of "
-                        f"{size} B host objects from {n} threads, PCIe-inclusive "
-                        "(pageable caller buffers; batching queue), this rank's device; "
-                        "GiB/s of object payload"}
-
+        srcs = np.ascontiguousarray(objs[:n, :size].cpu().numpy())
+        gpar = np.ascontiguousarray(parity[:n].cpu().numpy())
+        inproc = host_rates(self.le, srcs, gpar, size, bs, self.index, seconds)
+        inproc["link"] = self.link_rates()
+        inproc["link_busy"] = link_busy(inproc, inproc["link"], size, bs)
+        env = {k: v for k, v in os.environ.items()
+               if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
+                            "LEOEC_LIBRARY")}
+        env["LEOEC_NO_TORCH"] = "1"
+        with tempfile.TemporaryDirectory(prefix="leoec_host_") as d:
+            np.save(os.path.join(d, "srcs.npy"), srcs)
+            np.save(os.path.join(d, "gpar.npy"), gpar)
+            cmd = [sys.executable, os.path.abspath(__file__), "--host-child", "--host-data", d,
+                   "--pattern-device", str(self.index), "--size", str(size),
+                   "--host-seconds", str(seconds)]
+            try:
+                r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+                lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+                child = json.loads(lines[-1]) if r.returncode == 0 and lines else {
+                    "error": f"host child rc {r.returncode}: {r.stderr.strip()[-400:]}"}
+            except subprocess.TimeoutExpired:
+                child = {"error": f"host child timed out after {timeout} s"}
+        torch_rt = {k: inproc[k] for k in ("encode_GiBps", "decode_GiBps", "link", "link_busy",
+                                           "parity_vs_gpu")}
+        torch_rt["what"] = "the same leg in the bench process, on the torch wheel's HIP runtime"
+        if "error" in child:  # the in-process figures stand, with the child's failure named
+            out = dict(inproc)
+            out["runtime"] = "torch wheel's (the system-runtime child failed)"
+            out["child_error"] = child["error"]
+            return out
+        child["torch_runtime"] = torch_rt
+        return child
 
     def link_rates(self, mib=256, reps=5):
         """This device's PCIe copy rates from / to pinned host memory (GB/s,
-        median of `reps` copies of `mib` MiB): host -> device alone, device
-        -> host alone, and both directions at once on two streams (bytes of
-        both / time) — the link the host-memory leg runs on."""
+        median of `reps` copies of `mib` MiB) through torch: host -> device
+        alone, device -> host alone, and both directions at once on two
+        streams (bytes of both / time)."""
         t = self.torch
         n = mib << 20
         hsrc = t.empty(n, dtype=t.uint8, pin_memory=True)
@@ -398,11 +339,200 @@ class GpuBackend:
                "both_GBps": round(timed(True, True), 1),
                "what": f"pinned {mib} MiB copies, median of {reps}; both = the two directions "
                        "at once on two streams, bytes of both / time, on this process's HIP "
-                       "runtime (the torch wheel's, whose two copies do not overlap; the system "
-                       "runtime a NIF loads moves both at once at ~97 GB/s: DESIGN.md "
-                       "End-to-end)"}
+                       "runtime (the torch wheel's, whose two copies do not overlap)"}
         del hsrc, hdst, dsrc, ddst
         return out
+
+
+def host_rates(le, srcs, gpar, size, bs, device, seconds):
+    """host-memory leoec_encode / leoec_decode through the C ABI from one
+    thread per object of `srcs` (pageable numpy rows), back to back for
+    `seconds` per op, on `device` (leoec_host_spread([device]): the threads'
+    own current device would be device 0).  Checked, outside the timed loops:
+    every thread's encode parity equals `gpar` (the GPU's device parity of
+    its object) and every decode (data blocks ERASED lost) returns the
+    object.  No torch: bench.py runs it in the bench process and in the
+    system-runtime child (host_child)."""
+    import ctypes
+    import threading
+
+    import numpy as np
+    L = le.lib
+    n = srcs.shape[0]
+    srcs = [np.ascontiguousarray(srcs[t]) for t in range(n)]
+    filled = min(size // bs, K)
+    out_bytes = (K + M - filled) * bs
+    outs = [np.empty(out_bytes, dtype=np.uint8) for _ in range(n)]
+    decs = [np.empty(size, dtype=np.uint8) for _ in range(n)]
+    ids = list(range(len(ERASED), K + M))  # survivors: blocks 4..13
+    idv = (ctypes.c_int * len(ids))(*ids)
+
+    def block(t, i):
+        if i < filled:
+            return srcs[t].ctypes.data + i * bs
+        return outs[t].ctypes.data + (i - filled) * bs
+
+    def enc(t):
+        return L.leoec_encode(2, K, M, W, srcs[t].ctypes.data, size, outs[t].ctypes.data,
+                              out_bytes)
+
+    ptrs = []
+
+    def dec(t):
+        return L.leoec_decode(2, K, M, W, ptrs[t], idv, len(ids), bs, size,
+                              decs[t].ctypes.data)
+
+    def check():
+        enc_ok = all(np.array_equal(outs[t][(K - filled) * bs:], gpar[t]) for t in range(n))
+        dec_ok = all(np.array_equal(decs[t], srcs[t]) for t in range(n))
+        return enc_ok, dec_ok
+
+    def timed(fn):
+        errs, counts, box = [], [0] * n, {}
+        ready = threading.Barrier(n + 1)
+        go = threading.Event()
+
+        def work(t):
+            if fn(t) != 0:  # this thread's first call, outside the clock
+                errs.append(t)
+            ready.wait()
+            go.wait()
+            c = 0
+            while time.perf_counter() < box["end"]:
+                if fn(t) != 0:
+                    errs.append(t)
+                c += 1
+            counts[t] = c
+
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(n)]
+        for th in ths:
+            th.start()
+        ready.wait()
+        t0 = time.perf_counter()
+        box["end"] = t0 + seconds
+        go.set()
+        for th in ths:
+            th.join()
+        dt = time.perf_counter() - t0
+        if errs:
+            raise RuntimeError(f"host-path calls failed on threads {sorted(set(errs))[:8]}")
+        return sum(counts) * size / dt / 2**30, sum(counts)
+
+    le._lib.host_spread([device])
+    try:
+        for t in range(n):
+            if enc(t) != 0:
+                raise RuntimeError("leoec_encode failed")
+        ptrs[:] = [(ctypes.c_void_p * len(ids))(*[block(t, i) for i in ids]) for t in range(n)]
+        enc_gibs, enc_calls = timed(enc)
+        dec_gibs, dec_calls = timed(dec)
+        enc_ok, dec_ok = check()
+    finally:
+        le._lib.host_spread([])
+    return {"encode_GiBps": round(enc_gibs, 2), "decode_GiBps": round(dec_gibs, 2),
+            "callers": n, "seconds_per_op": seconds, "calls": [enc_calls, dec_calls],
+            "parity_vs_gpu": {"objects": n, "encode_equal": enc_ok, "decode_equal": dec_ok},
+            "what": f"C ABI leoec_encode / leoec_decode (data blocks {ERASED} lost) of "
+                    f"{size} B host objects from {n} threads, PCIe-inclusive "
+                    "(pageable caller buffers; batching queue), this rank's device; "
+                    "GiB/s of object payload"}
+
+
+def link_busy(rates, link, size, bs):
+    """The share of each second the op's bytes keep the link busy at the
+    one-direction copy rates measured alone (an encode: its object host ->
+    device, its m parity blocks back; a decode: its K survivors in, the
+    rebuilt blocks back); above 1 the two directions overlap."""
+    e = len(ERASED)
+    per = {"encode": (1.0, M * bs / size), "decode": (K * bs / size, e * bs / size)}
+    rate = {"encode": rates["encode_GiBps"], "decode": rates["decode_GiBps"]}
+    return {op: round(rate[op] * 2**30 / 1e9 * (h / link["h2d_GBps"] + d / link["d2h_GBps"]), 3)
+            for op, (h, d) in per.items()}
+
+
+def hip_link_rates(device, mib=256, reps=5):
+    """link_rates through the HIP runtime the process loaded (ctypes; the
+    system runtime in host_child): pinned hipHostMalloc buffers, two
+    runtime-created streams."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the one libleoec.so loaded
+    vp = ctypes.c_void_p
+    hip.hipMemcpyAsync.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
+    hip.hipStreamSynchronize.argtypes = [vp]
+    hip.hipHostFree.argtypes = [vp]
+    hip.hipFree.argtypes = [vp]
+    hip.hipStreamDestroy.argtypes = [vp]
+    n = mib << 20
+    if hip.hipSetDevice(device) != 0:
+        raise RuntimeError("hipSetDevice failed")
+    hs, hd, ds, dd, up, down = vp(), vp(), vp(), vp(), vp(), vp()
+    try:
+        for p in (hs, hd):
+            if hip.hipHostMalloc(ctypes.byref(p), ctypes.c_size_t(n), ctypes.c_uint(0)) != 0:
+                raise RuntimeError("hipHostMalloc failed")
+        for p in (ds, dd):
+            if hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(n)) != 0:
+                raise RuntimeError("hipMalloc failed")
+        for s in (up, down):
+            if hip.hipStreamCreateWithFlags(ctypes.byref(s), ctypes.c_uint(1)) != 0:
+                raise RuntimeError("hipStreamCreateWithFlags failed")
+        ctypes.memset(hs, 0x5A, n)
+        ctypes.memset(hd, 0, n)
+
+        def timed(h2d, d2h):
+            ms = []
+            for i in range(reps + 1):
+                t0 = time.perf_counter()
+                if h2d and hip.hipMemcpyAsync(ds, hs, n, 1, up) != 0:
+                    raise RuntimeError("hipMemcpyAsync failed")
+                if d2h and hip.hipMemcpyAsync(hd, dd, n, 2, down) != 0:
+                    raise RuntimeError("hipMemcpyAsync failed")
+                if hip.hipStreamSynchronize(up) != 0 or hip.hipStreamSynchronize(down) != 0:
+                    raise RuntimeError("hipStreamSynchronize failed")
+                if i:
+                    ms.append((time.perf_counter() - t0) * 1e3)
+            return round((h2d + d2h) * n / (sorted(ms)[len(ms) // 2] * 1e-3) / 1e9, 1)
+
+        return {"h2d_GBps": timed(True, False), "d2h_GBps": timed(False, True),
+                "both_GBps": timed(True, True),
+                "what": f"pinned {mib} MiB copies, median of {reps}; both = the two directions "
+                        "at once on two streams, bytes of both / time, system HIP runtime"}
+    finally:
+        for s in (up, down):
+            if s.value:
+                hip.hipStreamDestroy(s)
+        for p in (hs, hd):
+            if p.value:
+                hip.hipHostFree(p)
+        for p in (ds, dd):
+            if p.value:
+                hip.hipFree(p)
+
+
+def host_child(args):
+    """--host-child: a process without torch (LEOEC_NO_TORCH=1, set by the
+    parent), so libleoec.so runs on the system HIP runtime an Erlang VM
+    would load; host_rates over the parent's objects and GPU parity, the
+    link's copy rates on the same runtime, one JSON line."""
+    import numpy as np
+    if os.environ.get("LEOEC_NO_TORCH") != "1" or "torch" in sys.modules:
+        raise RuntimeError("host child must run without torch (LEOEC_NO_TORCH=1)")
+    import leo_erasure_amd as le
+    srcs = np.load(os.path.join(args.host_data, "srcs.npy"))
+    gpar = np.load(os.path.join(args.host_data, "gpar.npy"))
+    size = args.size
+    bs = ((size + K * W - 1) // (K * W) + 15) // 16 * 16 * W
+    if le.gf_init() != "ok":
+        raise RuntimeError("gf_init failed")
+    rec = host_rates(le, srcs, gpar, size, bs, args.pattern_device, args.host_seconds)
+    rec["link"] = hip_link_rates(args.pattern_device)
+    rec["link_busy"] = link_busy(rec, rec["link"], size, bs)
+    rec["runtime"] = ("system HIP runtime (/opt/rocm), child process without torch: what an "
+                      "Erlang VM loading the NIF gets")
+    if "torch" in sys.modules:
+        raise RuntimeError("torch was imported in the host child")
+    print(json.dumps(rec), flush=True)
+    return 0
 
 
 def pattern_child(args):
@@ -997,6 +1127,8 @@ def main(argv=None, backend=GpuBackend):
     args = parse(argv)
     if args.pattern_child:
         return pattern_child(args)
+    if args.host_child:
+        return host_child(args)
     if "WORLD_SIZE" not in os.environ:
         if args.gpus > 1:
             return launch_ranks(args, argv)

@@ -8,10 +8,16 @@ present the data-path calls return LEOEC_E_NO_DEVICE.
 import ctypes
 import os
 
-try:  # share torch's HIP runtime when torch is present (same soname, loaded first)
-    import torch  # noqa: F401
-except Exception:  # pragma: no cover - torch is optional for the host API
-    torch = None
+# Share torch's HIP runtime when torch is present (same soname, loaded
+# first).  LEOEC_NO_TORCH=1 keeps torch out of the process, so the library
+# binds the system runtime (its RUNPATH, /opt/rocm) as under an Erlang VM
+# loading the NIF: bench.py's host-memory leg runs in such a child process.
+torch = None
+if os.environ.get("LEOEC_NO_TORCH") != "1":
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is optional for the host API
+        torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libleoec.so")

@@ -539,6 +539,10 @@ struct Staging {
   bool zc = false;          // this call's device pointers are in [zd, zd + zcap)
   std::vector<uintptr_t> pins;  // registrations this call uses (pin_acquire), released
                                 // once its copies are done (pins_release)
+  hipStream_t up = nullptr;     // large_chunked: the H2D copies
+  hipStream_t down = nullptr;   //   and the D2H copies, beside `stream`'s launches
+  hipEvent_t ev_in[kStageSlots] = {};  // large_chunked: chunk c's H2D done
+  hipEvent_t ev_k[kStageSlots] = {};   //   chunk c's launch done
 
   Staging() = default;
   Staging(const Staging&) = delete;
@@ -554,7 +558,13 @@ struct Staging {
     if (device >= 0 && stream) {
       (void)hipSetDevice(device);
       (void)hipStreamSynchronize(stream);
+      for (hipStream_t x : {up, down})
+        if (x) (void)hipStreamSynchronize(x);
       for (hipEvent_t& e : ev)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
+      for (hipEvent_t& e : ev_in)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
+      for (hipEvent_t& e : ev_k)
         if (e) (void)hipEventDestroy(e), e = nullptr;
       if (buf) (void)hipFree(buf);
       if (ring) (void)hipHostFree(ring);
@@ -563,12 +573,14 @@ struct Staging {
         ResourcePool& p = g_pool[device];
         std::lock_guard<std::mutex> l(p.mu);
         p.streams.push_back(stream);
+        if (up) p.streams.push_back(up);
+        if (down) p.streams.push_back(down);
         if (zh && zcap <= kPoolMapped) p.mapped.push_back(ResourcePool::Mapped{zh, zd, zcap});
         else if (zh) (void)hipHostFree(zh);
       }
     }
     device = -1;
-    stream = nullptr;
+    stream = up = down = nullptr;
     buf = ring = hbuf = zh = zd = nullptr;
     cap = chunk = hcap = zcap = 0;
     zc = false;
@@ -1112,6 +1124,128 @@ int zc_chunked(const Plan& plan, Staging* st, const std::vector<ZcIn>& in,
   return LEOEC_OK;
 }
 
+// A per-thread call above the zero-copy cap (kGatherMax) in column chunks
+// with the link's two directions overlapped (round 5, Knobs::large_chunks).
+// The PCIe link is full duplex for DMA copies of pinned memory on separate
+// streams (97 GB/s for both directions against 57 for one), but not for
+// pageable copies, which the runtime stages through its own buffers (56 GB/s
+// for both: tools/duplex_probe.hip, profiles/r05_s28_duplex_caller_memory.log).
+// So the caller's input and output ranges are pinned in place (pin_acquire;
+// a range the runtime refuses to pin leaves the call to the one-piece copy
+// form) and chunk c of the GF(2^w) map — columns [c0, c1) of every block,
+// which depend only on the same columns of the inputs — moves as: its H2D
+// segments on the thread's input-copy stream, its launch on st->stream after
+// that copy's event, its D2H segments on the output-copy stream after the
+// launch's event, so chunk c's outputs return while chunk c + 1's inputs
+// arrive.  Device layout as the one-piece form: input i at st->buf + i *
+// stride, output o at st->buf + (nin + o) * stride.  `overlap` runs once
+// every chunk is issued.  *ran is false when the call is not split (the
+// knob, a non-GF plan, a zero-copy staging, blocks too small, no streams or
+// events, memory that cannot be pinned): the caller then takes the one-piece
+// path.  Measured and not shipped (Knobs::large_chunks = 1): registering the
+// caller's 140 MB of a 100 MiB encode per call costs more than the overlap
+// saves (2.73-3.08 ms at 4-8 chunks against 2.67-2.86 in one piece,
+// profiles/r05_s29_ref_chunks*.log).
+bool take_copy_stream(Staging* st, hipStream_t* s) {
+  if (*s) return true;
+  {
+    ResourcePool& p = g_pool[st->device];
+    std::lock_guard<std::mutex> l(p.mu);
+    if (!p.streams.empty()) {
+      *s = p.streams.back();
+      p.streams.pop_back();
+      return true;
+    }
+  }
+  if (hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess) {
+    *s = nullptr;
+    return false;
+  }
+  return true;
+}
+
+int large_chunked(const Plan& plan, Staging* st, const std::vector<ZcIn>& in,
+                  const std::vector<ZcOut>& out, uint64_t bs, uint64_t stride, bool* ran,
+                  void (*overlap)(void*) = nullptr, void* arg = nullptr) {
+  *ran = false;
+  const int want = std::min(knobs().large_chunks, kStageSlots);
+  if (want <= 1 || plan.kind != Plan::kGf || st->zc || !st->buf) return LEOEC_OK;
+  const uint64_t cw = round_to((bs + (uint64_t)want - 1) / (uint64_t)want, kZcChunkAlign);
+  if (cw >= bs) return LEOEC_OK;
+  const int nc = (int)((bs + cw - 1) / cw);
+  if (!take_copy_stream(st, &st->up) || !take_copy_stream(st, &st->down)) return LEOEC_OK;
+  for (int c = 0; c < nc; ++c)
+    for (hipEvent_t* e : {&st->ev_in[c], &st->ev_k[c]})
+      if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+        *e = nullptr;
+        return LEOEC_OK;
+      }
+  const int nin = (int)in.size(), nout = (int)out.size();
+  // pin every range (registration edges inside each: a copy never spans two)
+  std::vector<std::vector<uintptr_t>> cut_in(nin), cut_out(nout);
+  for (int i = 0; i < nin; ++i)
+    if (in[i].valid && !pin_acquire(st, in[i].host, (size_t)in[i].valid, &cut_in[i])) {
+      pins_release(st);
+      return LEOEC_OK;
+    }
+  for (int o = 0; o < nout; ++o)
+    if (out[o].n && !pin_acquire(st, out[o].host, (size_t)out[o].n, &cut_out[o])) {
+      pins_release(st);
+      return LEOEC_OK;
+    }
+  *ran = true;
+  // one copy of [h, h + n) of a pinned range, cut at its registration edges
+  auto copy = [](uint8_t* dev, uint8_t* host, size_t n, bool h2d, const std::vector<uintptr_t>& cuts,
+                 hipStream_t s) -> int {
+    const uintptr_t h = (uintptr_t)host;
+    size_t off = 0;
+    auto piece = [&](size_t stop) -> int {
+      if (stop <= off) return LEOEC_OK;
+      const hipError_t e = h2d ? hipMemcpyAsync(dev + off, host + off, stop - off, hipMemcpyHostToDevice, s)
+                               : hipMemcpyAsync(host + off, dev + off, stop - off, hipMemcpyDeviceToHost, s);
+      off = stop;
+      return hip_ok(e);
+    };
+    for (uintptr_t e : cuts)
+      if (e > h && e < h + n)
+        if (int rc = piece((size_t)(e - h))) return rc;
+    return piece(n);
+  };
+  int rc = LEOEC_OK;
+  for (int c = 0; c < nc && rc == LEOEC_OK; ++c) {
+    const uint64_t c0 = (uint64_t)c * cw, len = std::min(cw, bs - c0);
+    std::vector<Shard> si(nin), so(nout);
+    for (int i = 0; i < nin && rc == LEOEC_OK; ++i) {
+      const uint64_t v = in[i].valid > c0 ? std::min(in[i].valid - c0, len) : 0;
+      uint8_t* d = st->buf + (uint64_t)i * stride + c0;
+      if (v) rc = copy(d, const_cast<uint8_t*>(in[i].host) + c0, (size_t)v, true, cut_in[i], st->up);
+      si[i] = Shard{d, 0, v};
+    }
+    for (int o = 0; o < nout; ++o) so[o] = Shard{st->buf + (uint64_t)(nin + o) * stride + c0, 0, len};
+    if (rc == LEOEC_OK &&
+        (hipEventRecord(st->ev_in[c], st->up) != hipSuccess ||
+         hipStreamWaitEvent(st->stream, st->ev_in[c], 0) != hipSuccess))
+      rc = LEOEC_E_HIP;
+    if (rc == LEOEC_OK) rc = run_plan(plan, si, so, len, 1, st->stream);
+    if (rc == LEOEC_OK &&
+        (hipEventRecord(st->ev_k[c], st->stream) != hipSuccess ||
+         hipStreamWaitEvent(st->down, st->ev_k[c], 0) != hipSuccess))
+      rc = LEOEC_E_HIP;
+    for (int o = 0; o < nout && rc == LEOEC_OK; ++o) {
+      const uint64_t n = out[o].n > c0 ? std::min(out[o].n - c0, len) : 0;
+      if (n) rc = copy(const_cast<uint8_t*>(so[o].base), out[o].host + c0, (size_t)n, false, cut_out[o], st->down);
+    }
+  }
+  if (rc == LEOEC_OK && overlap) overlap(arg);  // the caller's host copies, while the chunks move
+  // every byte in host memory (or, after an error, nothing of the call in
+  // flight) before the pages are unpinned and the buffers reused
+  const hipError_t s1 = hipStreamSynchronize(st->up), s2 = hipStreamSynchronize(st->stream),
+                   s3 = hipStreamSynchronize(st->down);
+  pins_release(st);
+  if (rc == LEOEC_OK && (s1 != hipSuccess || s2 != hipSuccess || s3 != hipSuccess)) rc = LEOEC_E_HIP;
+  return rc;
+}
+
 // Stage the k survivor blocks, run the map into nwant device outputs (on the
 // calling thread's current device).  With `zouts` (the host destinations of
 // the outputs) a zero-copy call may run in column chunks (zc_chunked), which
@@ -1146,6 +1280,18 @@ int run_host_map(const Plan& plan, const uint8_t* const* blocks, const std::vect
       *dev_out = nullptr;
       *stride_out = bs16;
       return LEOEC_OK;
+    }
+  }
+  if (!zc && zouts) {  // above the zero-copy cap: column chunks, both directions at once
+    std::vector<ZcIn> zi(k);
+    for (int i = 0; i < k; ++i) zi[i] = ZcIn{blocks[slot[i]], bs};
+    bool ran;
+    rc = large_chunked(plan, st, zi, *zouts, bs16, bs16, &ran, overlap, arg);
+    if (rc || ran) {
+      *st_out = st;
+      *dev_out = nullptr;
+      *stride_out = bs16;
+      return rc;
     }
   }
   std::vector<Shard> in(k), out(want.size());
@@ -1258,14 +1404,16 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
   rc = stage_for((size_t)(k + m) * bs, &st, &zc);
   if (rc) return rc;
   uint8_t* base = zc ? st->zd : st->buf;
-  if (zc) {  // column chunks, when Knobs::zc_chunks asks for them
+  {  // column chunks: zero-copy (Knobs::zc_chunks) or, above its cap, DMA
+     // copies of pinned caller memory in both directions at once
+     // (Knobs::large_chunks)
     std::vector<ZcIn> zi(k);
     std::vector<ZcOut> zo(m);
     for (int j = 0; j < k; ++j)
       zi[j] = ZcIn{obj + (uint64_t)j * bs, clamp_valid(size, (uint64_t)j * bs, bs)};
     for (int i = 0; i < m; ++i) zo[i] = ZcOut{out + tail_bytes + (uint64_t)i * bs, bs};
     bool ran;
-    rc = zc_chunked(*plan, st, zi, zo, bs, bs, &ran);
+    rc = zc ? zc_chunked(*plan, st, zi, zo, bs, bs, &ran) : large_chunked(*plan, st, zi, zo, bs, bs, &ran);
     if (rc) st->zc = false;
     if (rc || ran) return rc;
   }

@@ -14,10 +14,7 @@ from . import _lib
 from ._lib import lib
 from .api import layout  # noqa: F401  (re-exported)
 
-try:
-    import torch
-except Exception:  # pragma: no cover
-    torch = None
+torch = _lib.torch  # (None under LEOEC_NO_TORCH=1: the device API then needs explicit streams)
 
 
 def _stream(stream):

@@ -198,6 +198,7 @@ int main(int argc, char** argv) {
         // targeted / broadcast wake-ups, flipped while callers wait in both forms
         leoec_measure_set_knob("LEOEC_HOSTQ_WAKE", (i / 5) % 2 ? "0" : "1");
         leoec_measure_set_knob("LEOEC_HOSTQ_STREAMS", (i / 7) % 2 ? "0" : "1");
+        leoec_measure_set_knob("LEOEC_LARGE_CHUNKS", i % 3 == 0 ? "1" : i % 3 == 1 ? "8" : "3");
         ++i;
         std::this_thread::sleep_for(std::chrono::milliseconds(3));
       }

@@ -114,6 +114,30 @@ def test_padding_10MiB_plus_1(gpu, le, oracle):
         _check_decode_subsets(le, cls, k, m, w, data, blocks, m, rng, limit=6)
 
 
+def test_host_objects_above_zero_copy_cap(gpu, le, oracle):
+    """Host calls whose span passes the 16 MiB zero-copy cap take the
+    per-thread copy path (one pageable copy each way; the measurement build's
+    column-chunked form is tested in test_measure_forms.py): encode, decode
+    of lost data blocks and repair of a data and a coding block, bit-exact
+    with the oracle, twice over the same buffers, for GF(2^8) / GF(2^16)
+    Reed-Solomon and ISA-L maps, a bitmatrix class and ragged sizes."""
+    for cls, k, m, w, size in [("vandrs", 10, 4, 8, (40 << 20) + 3), ("isars", 10, 4, 8, 24 << 20),
+                               ("vandrs", 6, 3, 16, (20 << 20) + 1001),
+                               ("cauchyrs", 10, 4, 8, (17 << 20) + 77)]:
+        data = rand_bytes(size, size % 997)
+        ref = oracle.encode(cls, k, m, w, data)
+        for _ in range(2):
+            st, blocks = le.nif_encode(cls, (k, m, w), data, size)
+            assert st == "ok" and blocks == ref, (cls, k, m, w, size)
+            ids = list(range(m, k + m))[::-1]
+            st, out = le.nif_decode(cls, (k, m, w), [ref[b] for b in ids], ids, size)
+            assert st == "ok" and out == data, (cls, k, m, w, size)
+            lost = [0, k + m - 1]
+            avail = [b for b in range(k + m) if b not in lost]
+            st, rep = le.nif_repair(cls, (k, m, w), [ref[b] for b in avail], avail, lost)
+            assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size)
+
+
 @pytest.mark.parametrize("km", [(10, 4), (8, 3), (6, 2), (4, 2), (4, 1)])
 def test_correctness_5MiB(gpu, le, km):
     """correctness_test (test/leo_erasure_tests.erl:171-204), default coder."""

@@ -143,6 +143,44 @@ int main(int argc, char** argv) {
                      for (int b = 0; b < kBatches; ++b)
                        CHECK(hipMemcpyAsync(din + slot_in(b), hin + slot_in(b), bin, hipMemcpyHostToDevice, s1));
                    }, -2});
+  // Caller memory (an Erlang binary is pageable): the same pair of copies
+  // from / to malloc'ed memory as is (the runtime stages it) and pinned in
+  // place with hipHostRegister.
+  unsigned char *pin_in = nullptr, *pin_out = nullptr, *pg_in = nullptr, *pg_out = nullptr;
+  if (posix_memalign((void**)&pin_in, 4096, bytes) || posix_memalign((void**)&pin_out, 4096, bytes) ||
+      posix_memalign((void**)&pg_in, 4096, bytes) || posix_memalign((void**)&pg_out, 4096, bytes))
+    return 1;
+  memset(pin_in, 0x5A, bytes);
+  memset(pin_out, 0, bytes);
+  memset(pg_in, 0x5A, bytes);
+  memset(pg_out, 0, bytes);
+  CHECK(hipHostRegister(pin_in, bytes, hipHostRegisterDefault));
+  CHECK(hipHostRegister(pin_out, bytes, hipHostRegisterDefault));
+  cases.push_back({"registered h2d", [&] { CHECK(hipMemcpyAsync(din, pin_in, bytes, hipMemcpyHostToDevice, s1)); }, 1});
+  cases.push_back({"registered h2d + registered d2h", [&] {
+                     CHECK(hipMemcpyAsync(din, pin_in, bytes, hipMemcpyHostToDevice, s1));
+                     CHECK(hipMemcpyAsync(pin_out, dout, bytes, hipMemcpyDeviceToHost, s2));
+                   }, 2});
+  cases.push_back({"pageable h2d", [&] { CHECK(hipMemcpyAsync(din, pg_in, bytes, hipMemcpyHostToDevice, s1)); }, 1});
+  cases.push_back({"pageable d2h", [&] { CHECK(hipMemcpyAsync(pg_out, dout, bytes, hipMemcpyDeviceToHost, s2)); }, 1});
+  cases.push_back({"pageable h2d + pageable d2h", [&] {
+                     CHECK(hipMemcpyAsync(din, pg_in, bytes, hipMemcpyHostToDevice, s1));
+                     CHECK(hipMemcpyAsync(pg_out, dout, bytes, hipMemcpyDeviceToHost, s2));
+                   }, 2});
+  // 8 chunks of 32 MiB from registered memory: each chunk's H2D on s1, its
+  // D2H on s2 after an event (the shape of a column-chunked large call)
+  constexpr int kCh = 8;
+  hipEvent_t ch_ev[kCh];
+  for (auto& e : ch_ev) CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  cases.push_back({"registered, 8 chunks: h2d(c) || d2h(c-1)", [&] {
+                     const size_t cb = bytes / kCh;
+                     for (int c = 0; c < kCh; ++c) {
+                       CHECK(hipMemcpyAsync(din + c * cb, pin_in + c * cb, cb, hipMemcpyHostToDevice, s1));
+                       CHECK(hipEventRecord(ch_ev[c], s1));
+                       CHECK(hipStreamWaitEvent(s2, ch_ev[c], 0));
+                       CHECK(hipMemcpyAsync(pin_out + c * cb, dout + c * cb, cb, hipMemcpyDeviceToHost, s2));
+                     }
+                   }, 2});
   printf("# %zu MiB per direction, %d reps, kernel grid %d x 256 lanes\n", mib, reps, wgs);
   for (auto& c : cases) {
     c.run();  // warm-up
