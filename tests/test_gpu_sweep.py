@@ -9,7 +9,6 @@ from one byte to 3 MiB, random survivor orders and erasure sets).
 """
 import random
 
-import numpy as np
 import pytest
 
 from gpu_helpers import batch as _batch
