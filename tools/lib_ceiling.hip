@@ -129,6 +129,80 @@ pattern(const unsigned char* __restrict__ in, unsigned char* __restrict__ out, G
   }
 }
 
+// FORM sweep (round 5, session 33): line-aligned loads with the packets'
+// misalignment undone in the lanes.  A 64-lane wave sweeps ST consecutive
+// 1 KiB tiles of every packet.  Packet q (block j, packet x) starts delta_q
+// = (address mod 128) bytes into a line; its tile t needs the bytes
+// [t*1024, +1024) = V_t[delta:] ++ V_{t+1}[:delta] of the LINE-ALIGNED
+// windows V_t = [start - delta + t*1024, +1024): each window is loaded once
+// (8 lines, not 9), the previous one kept in VGPRs (`carry`), and the lane
+// rotation by delta / 16 lanes goes through a 2 KiB LDS scratch (ds_write of
+// both windows, ds_read at the offset; one wave per workgroup, so in order
+// without a barrier).  LA: packets of look-ahead for the next windows.
+template <int K, int ST, int LA>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 8)))
+sweep(const unsigned char* __restrict__ in, unsigned char* __restrict__ out, Geo g) {
+  constexpr int NP = K * W;
+  __shared__ u4 scratch[128];
+  const unsigned nsw = (g.tiles + ST - 1) / ST;
+  const unsigned b = obj_map(blockIdx.x, gridDim.x, nsw);
+  const unsigned obj = b / nsw, sw = b % nsw;
+  const unsigned tb = sw * ST, te = tb + ST < g.tiles ? tb + ST : g.tiles;
+  const unsigned lane = threadIdx.x;
+  const unsigned char* ib = in + (size_t)obj * g.row;
+  unsigned char* ob = out + (size_t)obj * 2 * g.bs;
+  // per packet: its line-aligned start (as an offset in the object row,
+  // which starts on a line) and its shift in 16-B lanes
+  auto aligned_at = [&](int q) -> unsigned {
+    const unsigned a = (unsigned)(q / W) * g.bs + (unsigned)(q % W) * g.ps;
+    return a & ~127u;
+  };
+  auto shift = [&](int q) -> unsigned {
+    const unsigned a = (unsigned)(q / W) * g.bs + (unsigned)(q % W) * g.ps;
+    return (a & 127u) / 16u;
+  };
+  const auto rs = rsrc(ib, (unsigned)g.row);  // past the row: zeros
+  auto load = [&](int q, unsigned t) -> u4 {
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, aligned_at(q) + t * 1024u + lane * 16u, 0, 2);
+  };
+  u4 carry[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) carry[q] = load(q, tb);
+  for (unsigned t = tb; t < te; ++t) {
+    u4 P[W], Q[W];
+#pragma unroll
+    for (int x = 0; x < W; ++x) P[x] = Q[x] = u4{0u, 0u, 0u, 0u};
+    u4 ring[LA + 1];
+#pragma unroll
+    for (int q = 0; q < LA; ++q) ring[q] = load(q, t + 1);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      if (q + LA < NP) ring[(q + LA) % (LA + 1)] = load(q + LA, t + 1);
+      const u4 nxt = ring[q % (LA + 1)];
+      scratch[lane] = carry[q];
+      scratch[64 + lane] = nxt;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      const u4 v = scratch[lane + shift(q)];
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      carry[q] = nxt;
+      const int x = q % W;
+      P[x] ^= v;
+      Q[x] ^= v;
+      pin(P[x]);
+      pin(Q[x]);
+    }
+    const unsigned off = t * 1024u + lane * 16u;
+    if (off < g.ps) {
+#pragma unroll
+      for (int x = 0; x < W; ++x) {
+        unsigned char* p = ob + (size_t)x * g.ps + off;
+        __builtin_nontemporal_store(P[x], reinterpret_cast<u4*>(p));
+        __builtin_nontemporal_store(Q[x], reinterpret_cast<u4*>(p + g.bs));
+      }
+    }
+  }
+}
+
 // A flat streaming kernel over the same bytes: lane l of tile t reads 16 B
 // at t * TW * 16 + l * 16 of each of the K data blocks (blocks as flat
 // rows, no packets) and writes the XOR to both output blocks.
@@ -165,6 +239,7 @@ struct Case {
   KFn k;
   unsigned tw;
   bool aligned;
+  unsigned st = 0;  // sweep form: tiles per wave (grid = objects x ceil(tiles / st))
 };
 
 template <int K>
@@ -193,6 +268,7 @@ int run(unsigned nobj, int reps) {
   hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, (unsigned*)in, in_bytes / 4, 7u);
   CHECK(hipDeviceSynchronize());
 #define PC(F, LA, TW) reinterpret_cast<KFn>(&pattern<K, F, LA, TW>)
+#define SW(ST, LA) reinterpret_cast<KFn>(&sweep<K, ST, LA>)
   std::vector<Case> cases = {
       {"branchy la2 wg64 (shipped lib_apply's load shape)", PC(0, 2, 64), 64, false},
       {"ring la2 wg64 (libb_apply)", PC(1, 2, 64), 64, false},
@@ -206,6 +282,10 @@ int run(unsigned nobj, int reps) {
       {"ring la2 wg64, aligned packets", PC(1, 2, 64), 64, true},
       {"ring la4 wg64, aligned packets", PC(1, 4, 64), 64, true},
       {"block wg64, aligned packets", PC(2, 0, 64), 64, true},
+      {"sweep 4 tiles la2 (aligned loads, lanes rotated via LDS)", SW(4, 2), 64, false, 4},
+      {"sweep 8 tiles la2", SW(8, 2), 64, false, 8},
+      {"sweep 8 tiles la4", SW(8, 4), 64, false, 8},
+      {"sweep 16 tiles la2", SW(16, 2), 64, false, 16},
   };
   // every packet form computes the same XORs: outputs compared with the
   // first form's, byte for byte, on the reference geometry
@@ -216,8 +296,9 @@ int run(unsigned nobj, int reps) {
       Geo g = ref;
       g.tiles = (g.ps + cases[c].tw * 16 - 1) / (cases[c].tw * 16);
       g.full_tiles = g.ps / (cases[c].tw * 16);
+      const unsigned grid = cases[c].st ? (g.tiles + cases[c].st - 1) / cases[c].st : g.tiles;
       CHECK(hipMemset(out, 0, out_bytes));
-      hipLaunchKernelGGL(cases[c].k, dim3(nobj * g.tiles), dim3(cases[c].tw), 0, 0, in, out, g);
+      hipLaunchKernelGGL(cases[c].k, dim3(nobj * grid), dim3(cases[c].tw), 0, 0, in, out, g);
       CHECK(hipMemcpy(c == 0 ? a.data() : b.data(), out, out_bytes, hipMemcpyDeviceToHost));
       if (c && a != b) {
         printf("# form %s: output differs from the branchy form\n", cases[c].name.c_str());
@@ -239,7 +320,8 @@ int run(unsigned nobj, int reps) {
         g.full_tiles = g.ps / (cases[c].tw * 16);
         const KFn k = cases[c].k;
         const unsigned tw = cases[c].tw;
-        launch = [=]() { hipLaunchKernelGGL(k, dim3(nobj * g.tiles), dim3(tw), 0, 0, in, out, g); };
+        const unsigned grid = cases[c].st ? (g.tiles + cases[c].st - 1) / cases[c].st : g.tiles;
+        launch = [=]() { hipLaunchKernelGGL(k, dim3(nobj * grid), dim3(tw), 0, 0, in, out, g); };
       } else {
         const unsigned tw = c == cases.size() ? 64 : 256;
         const unsigned ft = (g.bs + tw * 16 - 1) / (tw * 16);
