@@ -10,12 +10,17 @@
 // {K,M,W} arity is checked, and the NIFs run on dirty schedulers so a GPU
 // round trip never blocks a normal scheduler thread.
 //
-// load/3 (the reference has none, nif.cpp:353): the library runs a
-// host-memory call on the calling scheduler thread's current HIP device.  A
-// VM that should drive several GPUs sets LEOEC_HOST_DEVICES before starting
-// ("all", or a comma list of device ordinals): load passes the set to
-// leoec_host_spread (which warms every device of the set before returning),
-// and calls then go to the least-loaded device of the set.  A malformed
+// load/3 (the reference has none, nif.cpp:353): the library alone runs a
+// host-memory call on the calling scheduler thread's current HIP device,
+// which for every scheduler of a VM is device 0.  So the shim spreads the
+// VM's calls over every gfx950 device it can see by default (round 5; one
+// VM per GPU, started with HIP_VISIBLE_DEVICES, sees just its own), and
+// LEOEC_HOST_DEVICES overrides that before the VM starts: "all" (the
+// default), a comma list of device ordinals, or "current" / "" for no
+// spreading (each call on its scheduler thread's current device, the
+// library's own rule).  load passes the set to leoec_host_spread (which
+// warms every device of the set before returning), and calls then go to
+// the least-loaded device of the set.  A malformed
 // value fails the load, and so does a well-formed set naming a device the
 // process cannot use (say "0,1,7" on a 2-GPU node: leoec_host_spread refuses
 // it and would leave every call on the scheduler thread's current device);
@@ -225,11 +230,13 @@ ErlNifFunc nif_funcs[] = {
     {"repair", 5, nif_repair, ERL_NIF_DIRTY_JOB_IO_BOUND},
 };
 
-// LEOEC_HOST_DEVICES -> devices; false if malformed.  Unset or empty: no
-// spreading (an empty set).
+// LEOEC_HOST_DEVICES -> devices; false if malformed.  Unset: "all" (every
+// gfx950 device of the process); "" or "current": no spreading (an empty
+// set).
 bool parse_host_devices(const char* e, std::vector<int>* devs) {
   devs->clear();
-  if (!e || !*e) return true;
+  if (!e) e = "all";
+  if (!*e || !std::strcmp(e, "current")) return true;
   if (!std::strcmp(e, "all")) {
     const int n = leoec_host_lanes(nullptr, 0);
     if (n > 0) {

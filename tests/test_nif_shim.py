@@ -345,15 +345,17 @@ def _load_with(nif, spec):
     return int(out.stdout.strip().splitlines()[-1]), out.stderr
 
 
-@pytest.mark.parametrize("spec,rc", [(None, 0), ("", 0), ("all", 0), ("0", 0), ("0,1,7", 0),
-                                     ("0,x", 1), (",", 1), ("1,", 1), ("-1", 1), ("gpu0", 1)])
+@pytest.mark.parametrize("spec,rc", [(None, 0), ("", 0), ("current", 0), ("all", 0), ("0", 0),
+                                     ("0,1,7", 0), ("0,x", 1), (",", 1), ("1,", 1), ("-1", 1),
+                                     ("gpu0", 1), ("Current", 1)])
 def test_load_host_devices(nif, spec, rc):
-    """The shim's load callback (the reference registers none): the
-    LEOEC_HOST_DEVICES opt-in to spreading host calls over several GPUs is
-    parsed at load; a malformed value fails the load, a well-formed one that
-    the runtime cannot serve (no GPU here) is left to the data calls.  Run in
-    a child process: the test never writes its own environment."""
-    if spec not in (None, "", "0,x", ",", "1,", "-1", "gpu0"):
+    """The shim's load callback (the reference registers none): host calls
+    spread over every gfx950 device by default (unset = "all"),
+    LEOEC_HOST_DEVICES picks a set or "current" / "" for none; it is parsed
+    at load, a malformed value fails the load, a well-formed one that the
+    runtime cannot serve (no GPU here) is left to the data calls.  Run in a
+    child process: the test never writes its own environment."""
+    if spec not in ("", "current", "0,x", ",", "1,", "-1", "gpu0", "Current"):
         import leo_erasure_amd as le
         if le.lib.leoec_host_lanes(None, 0) > 0:
             pytest.skip("a GPU is present: test_load_host_devices_on_gpu")
@@ -361,7 +363,8 @@ def test_load_host_devices(nif, spec, rc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("spec,rc", [("all", 0), ("0", 0), ("0,63", 2), ("63", 2)])
+@pytest.mark.parametrize("spec,rc", [(None, 0), ("all", 0), ("current", 0), ("0", 0),
+                                     ("0,63", 2), ("63", 2)])
 def test_load_host_devices_on_gpu(nif, spec, rc):
     """With a GPU present, a well-formed LEOEC_HOST_DEVICES naming a device
     the process cannot use fails the load (exit status 2, message on stderr)
