@@ -775,7 +775,7 @@ bool pin_acquire(Staging* st, const void* p, size_t n, std::vector<uintptr_t>* c
   if (cur < hi) gaps.emplace_back(cur, hi);
   for (size_t g = 0; g < gaps.size(); ++g) {
     if (hipHostRegister(reinterpret_cast<void*>(gaps[g].first), gaps[g].second - gaps[g].first,
-                        hipHostRegisterPortable) != hipSuccess) {
+                        hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
       (void)hipGetLastError();
       for (size_t u = 0; u < g; ++u) (void)hipHostUnregister(reinterpret_cast<void*>(gaps[u].first));
       return false;
@@ -1124,6 +1124,84 @@ int zc_chunked(const Plan& plan, Staging* st, const std::vector<ZcIn>& in,
   return LEOEC_OK;
 }
 
+// A per-thread zero-copy call with the caller's blocks pinned in place
+// (round 5, Knobs::zc_pin): the kernel reads the caller's input blocks and
+// writes the caller's output blocks where they are, over PCIe, instead of
+// the call packing its inputs into the thread's mapped buffer and unpacking
+// its outputs (tools/register_probe.hip, profiles/r05_s35_register_probe.log:
+// at 1 MiB, pack 40 us against hipHostRegister + device pointer +
+// unregister 1.5 us, and the kernel's read 42 us against 38 from the mapped
+// buffer).  Inputs and outputs are pinned through the registry (pin_acquire:
+// page-granular, shared between concurrent calls on one binary), each block
+// must start on 16 bytes (the kernels' alignment) and the runtime must give a
+// device address for it; otherwise *ran is false and the caller packs.
+// Measured and not shipped (Knobs::zc_pin = 0): the probe's 1.5 us of
+// registration did not carry over to calls — a lone 1 MiB call 71.6-72.4 us
+// against 71.2-81.6 packed — and concurrent callers serialise on it (2-8
+// callers 15-18 GiB/s against 20-40: profiles/r05_s36_few_pin*.log).
+// A kernel's last 16-byte chunk of a block may read up to 15 bytes past its
+// valid length: that chunk lies in the page of the block's last byte, which
+// is pinned; stores never pass `n`.  `overlap` runs while the kernel does.
+int zc_in_place(const Plan& plan, Staging* st, const std::vector<ZcIn>& in,
+                const std::vector<ZcOut>& out, uint64_t bs, bool* ran,
+                void (*overlap)(void*) = nullptr, void* arg = nullptr) {
+  *ran = false;
+  if (!knobs().zc_pin) return LEOEC_OK;
+  for (const ZcIn& z : in)
+    if (z.valid && ((uintptr_t)z.host & 15u)) return LEOEC_OK;
+  for (const ZcOut& z : out)
+    if (z.n && ((uintptr_t)z.host & 15u)) return LEOEC_OK;
+  std::vector<uintptr_t> cuts;  // (copies only: a kernel may span registrations)
+  auto dev_addr = [](const void* h, uint8_t** d) {
+    void* p = nullptr;
+    if (hipHostGetDevicePointer(&p, const_cast<void*>(h), 0) != hipSuccess || !p) {
+      (void)hipGetLastError();
+      return false;
+    }
+    *d = static_cast<uint8_t*>(p);
+    return true;
+  };
+  std::vector<Shard> si(in.size()), so(out.size());
+  for (size_t i = 0; i < in.size(); ++i) {
+    uint8_t* d = nullptr;
+    if (in[i].valid && (!pin_acquire(st, in[i].host, (size_t)in[i].valid, &cuts) ||
+                        !dev_addr(in[i].host, &d))) {
+      pins_release(st);
+      return LEOEC_OK;
+    }
+    si[i] = Shard{d, 0, in[i].valid};
+  }
+  for (size_t o = 0; o < out.size(); ++o) {
+    uint8_t* d = nullptr;
+    if (out[o].n && (!pin_acquire(st, out[o].host, (size_t)out[o].n, &cuts) ||
+                     !dev_addr(out[o].host, &d))) {
+      pins_release(st);
+      return LEOEC_OK;
+    }
+    so[o] = Shard{d, 0, out[o].n};
+  }
+  // a block with nothing valid (past the object's end) reads as zeros; its
+  // shard still gets an address the device can see
+  const uint8_t* any = nullptr;
+  for (const Shard& x : si)
+    if (x.base) any = x.base;
+  for (const Shard& x : so)
+    if (x.base) any = x.base;
+  if (!any) return LEOEC_OK;  // (nothing pinned: no blocks at all)
+  for (Shard& x : si)
+    if (!x.base) x.base = any;
+  for (Shard& x : so)
+    if (!x.base) x.base = any;
+  *ran = true;
+  int rc = run_plan(plan, si, so, bs, 1, st->stream);
+  if (rc == LEOEC_OK && overlap) overlap(arg);
+  const hipError_t e = hipStreamSynchronize(st->stream);
+  pins_release(st);
+  if (rc == LEOEC_OK && e != hipSuccess) rc = LEOEC_E_HIP;
+  st->zc = false;
+  return rc;
+}
+
 // A per-thread call above the zero-copy cap (kGatherMax) in column chunks
 // with the link's two directions overlapped (round 5, Knobs::large_chunks).
 // The PCIe link is full duplex for DMA copies of pinned memory on separate
@@ -1269,8 +1347,9 @@ int run_host_map(const Plan& plan, const uint8_t* const* blocks, const std::vect
   if (zc && zouts) {
     std::vector<ZcIn> zi(k);
     for (int i = 0; i < k; ++i) zi[i] = ZcIn{blocks[slot[i]], bs};
-    bool ran;
-    rc = zc_chunked(plan, st, zi, *zouts, bs16, bs16, &ran, overlap, arg);
+    bool ran = false;
+    rc = zc_in_place(plan, st, zi, *zouts, bs16, &ran, overlap, arg);
+    if (rc == LEOEC_OK && !ran) rc = zc_chunked(plan, st, zi, *zouts, bs16, bs16, &ran, overlap, arg);
     if (rc) {
       st->zc = false;
       return rc;
@@ -1412,8 +1491,10 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
     for (int j = 0; j < k; ++j)
       zi[j] = ZcIn{obj + (uint64_t)j * bs, clamp_valid(size, (uint64_t)j * bs, bs)};
     for (int i = 0; i < m; ++i) zo[i] = ZcOut{out + tail_bytes + (uint64_t)i * bs, bs};
-    bool ran;
-    rc = zc ? zc_chunked(*plan, st, zi, zo, bs, bs, &ran) : large_chunked(*plan, st, zi, zo, bs, bs, &ran);
+    bool ran = false;
+    if (zc) rc = zc_in_place(*plan, st, zi, zo, bs, &ran);  // the caller's blocks, pinned in place
+    if (rc == LEOEC_OK && !ran)
+      rc = zc ? zc_chunked(*plan, st, zi, zo, bs, bs, &ran) : large_chunked(*plan, st, zi, zo, bs, bs, &ran);
     if (rc) st->zc = false;
     if (rc || ran) return rc;
   }

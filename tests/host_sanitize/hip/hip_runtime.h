@@ -61,6 +61,7 @@ typedef enum hipMemcpyKind {
 #define hipHostMallocMapped 0x2
 #define hipHostRegisterDefault 0x0
 #define hipHostRegisterPortable 0x1
+#define hipHostRegisterMapped 0x2
 
 struct hipDeviceProp_t {
   char name[256];
@@ -248,6 +249,11 @@ inline hipError_t hipHostFree(void* p) {
   return hipSuccess;
 }
 inline hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned) {
+  // only pinned memory (hipHostMalloc, hipHostRegister) has a device address
+  if (!fakehip::pinned().contains(h, 1)) {
+    *d = nullptr;
+    return hipErrorInvalidValue;
+  }
   *d = h;
   return hipSuccess;
 }

@@ -199,6 +199,7 @@ int main(int argc, char** argv) {
         leoec_measure_set_knob("LEOEC_HOSTQ_WAKE", (i / 5) % 2 ? "0" : "1");
         leoec_measure_set_knob("LEOEC_HOSTQ_STREAMS", (i / 7) % 2 ? "0" : "1");
         leoec_measure_set_knob("LEOEC_LARGE_CHUNKS", i % 3 == 0 ? "1" : i % 3 == 1 ? "8" : "3");
+        leoec_measure_set_knob("LEOEC_ZC_PIN", (i / 11) % 2 ? "0" : "1");
         ++i;
         std::this_thread::sleep_for(std::chrono::milliseconds(3));
       }
@@ -234,7 +235,8 @@ int main(int argc, char** argv) {
       fail("data calls built queues after the warm-up: " + std::to_string(q));
   }
 
-  // phase 2b: a per-thread zero-copy call whose second column chunk cannot
+  // phase 2b: a per-thread zero-copy call (packed: its object is not on a
+  // 16-byte boundary) whose second column chunk cannot
   // get its event (the n-th hipEventCreateWithFlags of the thread fails):
   // the call reports LEOEC_E_HIP having drained chunk 0, which reads and
   // writes the thread's mapped buffer, so the thread's next call — which
@@ -246,9 +248,14 @@ int main(int argc, char** argv) {
     Case d{LEOEC_VANDRS, 10, 4, 8, 262144};
     prepare(&d, 32);
     std::thread t([&] {
+      // the object 8 bytes past a 16-byte boundary: the in-place form
+      // (zc_in_place) declines it, so the call takes the packed column chunks
+      std::vector<uint8_t> shifted(c.size + 32);
+      uint8_t* src = shifted.data() + ((24 - ((uintptr_t)shifted.data() & 15u)) & 15u);
+      std::memcpy(src, c.data.data(), c.size);
       fakehip::fail_nth_event_create(2);
       std::vector<uint8_t> out((size_t)(c.k + c.m - c.filled) * c.bs);
-      const int rc = leoec_encode(c.coding, c.k, c.m, c.w, c.data.data(), c.size, out.data(),
+      const int rc = leoec_encode(c.coding, c.k, c.m, c.w, src, c.size, out.data(),
                                   out.size());
       const int left = fakehip::fail_event_create_in();
       fakehip::fail_nth_event_create(0);

@@ -395,7 +395,8 @@ def test_host_staging_forms(gpu, le, oracle, staging, chunk_kib, measure):
         lost = [0, k + m - 1] if m > 1 else [0]
         avail = [b for b in range(k + m) if b not in lost]
         st, rep = le.nif_repair(cls, (k, m, w), [ref[b] for b in avail], avail, lost)
-        assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size)
+        assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size,
+                                                              rep if st != "ok" else "")
 
 
 @pytest.mark.parametrize("chunks", ["2", "3", "8"])
@@ -451,7 +452,8 @@ def test_host_large_chunked(gpu, le, oracle, chunks, measure):
             lost = [0, k + m - 1]
             avail = [b for b in range(k + m) if b not in lost]
             st, rep = le.nif_repair(cls, (k, m, w), [ref[b] for b in avail], avail, lost)
-            assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size)
+            assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size,
+                                                                  rep if st != "ok" else "")
 
 
 @pytest.mark.parametrize("pin_kib", ["0", "512", "5120"])
@@ -480,7 +482,8 @@ def test_host_pinned_large_objects(gpu, le, oracle, pin_kib, measure):
             lost = [0, k + m - 1]
             avail = [b for b in range(k + m) if b not in lost]
             st, rep = le.nif_repair(cls, (k, m, w), [ref[b] for b in avail], avail, lost)
-            assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size)
+            assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size,
+                                                                  rep if st != "ok" else "")
 
 
 @pytest.mark.parametrize("form", ["always-batch", "per-thread", "lanes4",

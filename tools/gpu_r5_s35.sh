@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 5, session 35: a lone call's pack / unpack against pinning the
+# caller's memory in place (tools/register_probe.hip).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p $OUT
+step() { local name=$1 t=$2; shift 2; echo "=== $name"; timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "=== $name rc=$rc"; tail -n ${TAILN:-3} "$OUT/$name.log"; if [ $rc -ne 0 ]; then exit $rc; fi; }
+TAILN=5 step r05_s35_register_probe 180 tools/register_probe 200
+echo "session done"
