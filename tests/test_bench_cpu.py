@@ -199,3 +199,28 @@ def test_headline_is_the_faster_parity_equal_leg(port, ref, top):
     assert rec["structure"] == ("ISA-L" if top == "isa_l_port" else "Jerasure")
     assert rec["cores"] == 15 and rec["pinning"] == {"cpus": [0]}
     assert rec["full_share_estimate_GiBps"] == pytest.approx(want[top] * 16 / 15, rel=1e-3)
+
+
+def test_link_busy_counts_both_directions():
+    """bench.link_busy: the share of a second an op's bytes keep the link
+    busy at the one-direction rates (an encode moves its object in and m
+    parity blocks out); 1.0 = serial copies back to back, above 1 the two
+    directions overlap (the batching queue's copy streams)."""
+    size, bs = 1 << 20, 104960
+    link = {"h2d_GBps": 50.0, "d2h_GBps": 50.0}
+    # encode at the rate where the object's bytes alone fill the H2D direction
+    full_in = 50e9 / 2**30  # GiB/s of payload whose input bytes take 1 s per second
+    busy = bench.link_busy({"encode_GiBps": full_in, "decode_GiBps": full_in}, link, size, bs)
+    assert busy["encode"] == pytest.approx(1.0 + bench.M * bs / size, rel=1e-3)
+    assert busy["decode"] == pytest.approx((bench.K + len(bench.ERASED)) * bs / size, rel=1e-3)
+
+
+def test_host_child_refuses_torch(monkeypatch):
+    """The host leg's child must run on the system HIP runtime: it refuses
+    to run in a process that has torch (LEOEC_NO_TORCH unset)."""
+    monkeypatch.delenv("LEOEC_NO_TORCH", raising=False)
+
+    class A:
+        host_data, size, pattern_device, host_seconds = "", 1 << 20, 0, 0.1
+    with pytest.raises(RuntimeError, match="without torch"):
+        bench.host_child(A())
