@@ -185,7 +185,9 @@ int launch_slot(Slot* s) {
   const bool zc = knobs().hostq_zc != 0;
   uint8_t* din = zc ? s->z_in : s->d_in;
   uint8_t* dout = zc ? s->z_out : s->d_out;
-  const bool split = !zc && knobs().hostq_streams == 1 && s->up && s->down;
+  // (small batches stay on the slot's stream: Knobs::hostq_split_kib)
+  const bool split = !zc && knobs().hostq_streams == 1 && s->up && s->down &&
+                     s->used_in >= ((uint64_t)knobs().hostq_split_kib << 10);
   hipStream_t cin = split ? s->up : s->stream;     // the input copy's stream
   hipStream_t cout = split ? s->down : s->stream;  // the output copy's stream
   int rc = zc ? LEOEC_OK

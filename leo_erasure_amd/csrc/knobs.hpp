@@ -48,6 +48,10 @@ struct Knobs {
   int hostq_depth = 3;       // LEOEC_HOSTQ_DEPTH: batches on the GPU at once
   int hostq_streams = 1;     // LEOEC_HOSTQ_STREAMS: 1 a batch's H2D / D2H on the queue's two copy
                              // streams (shipped), 0 everything on the slot's stream
+  int hostq_split_kib = 1024;  // LEOEC_HOSTQ_SPLIT_KIB: batches with less input than this stay on
+                             // the slot's stream (their cross-stream events cost more than the
+                             // link's overlap gives: 16 / 64 KiB objects -5 % split,
+                             // profiles/r05_s39_small_streams*.log)
   int hostq_sync = 1;        // LEOEC_HOSTQ_SYNC: 1 poll events (hipEventQuery + yield),
                              //   0 hipEventSynchronize, 2 the same on blocking-sync events
   int hostq_close = 1;       // LEOEC_HOSTQ_CLOSE: 1 close a batch when the previous H2D is

@@ -198,6 +198,7 @@ int main(int argc, char** argv) {
         // targeted / broadcast wake-ups, flipped while callers wait in both forms
         leoec_measure_set_knob("LEOEC_HOSTQ_WAKE", (i / 5) % 2 ? "0" : "1");
         leoec_measure_set_knob("LEOEC_HOSTQ_STREAMS", (i / 7) % 2 ? "0" : "1");
+        leoec_measure_set_knob("LEOEC_HOSTQ_SPLIT_KIB", i % 2 ? "0" : "1024");
         leoec_measure_set_knob("LEOEC_LARGE_CHUNKS", i % 3 == 0 ? "1" : i % 3 == 1 ? "8" : "3");
         leoec_measure_set_knob("LEOEC_ZC_PIN", (i / 11) % 2 ? "0" : "1");
         ++i;
