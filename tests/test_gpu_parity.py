@@ -608,3 +608,26 @@ def test_host_spread_warms_its_devices(gpu):
     assert out["ok"] and out["parity"]
     # a cold first call pays ~150-250 ms of runtime and queue set-up
     assert out["t_first"] < 0.05, out
+
+
+def test_bench_host_leg_on_the_system_runtime(gpu):
+    """bench.py's host-memory leg runs in a torch-free child process, so
+    libleoec.so binds the system HIP runtime an Erlang VM would load; its
+    record carries that runtime, outputs equal to the GPU's device parity,
+    and the bench process's own (torch-runtime) figures beside it."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LEOEC_LIBRARY")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--objects", "64",
+                        "--steps", "2", "--warmup", "1", "--warmup-s", "0.1", "--no-cpu",
+                        "--no-ceiling", "--host-callers", "8", "--host-seconds", "0.2"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["verified"] is True
+    hp = rec["host_path"]["per_rank"][0]
+    assert "child_error" not in hp, hp.get("child_error")
+    assert hp["runtime"].startswith("system HIP runtime")
+    assert hp["parity_vs_gpu"] == {"objects": 8, "encode_equal": True, "decode_equal": True}
+    assert hp["encode_GiBps"] > 0 and hp["decode_GiBps"] > 0
+    assert hp["torch_runtime"]["parity_vs_gpu"]["encode_equal"] is True
