@@ -101,6 +101,9 @@ def _load(path=LIB_PATH):
     if hasattr(L, "leoec_measure_warm_state"):
         L.leoec_measure_warm_state.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.leoec_measure_warm_state.restype = None
+    if hasattr(L, "leoec_measure_reclaim_state"):
+        L.leoec_measure_reclaim_state.argtypes = [ctypes.POINTER(ctypes.c_long)]
+        L.leoec_measure_reclaim_state.restype = None
     if hasattr(L, "leoec_measure_xor_pattern_dev"):  # measurement build (xor_pattern.hip)
         L.leoec_measure_xor_pattern_dev.argtypes = [
             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
@@ -186,6 +189,18 @@ def measure_warm_state(dev):
     _current.leoec_measure_warm_state(dev, out)
     return {"pool_streams": out[0], "pool_mapped": out[1], "queue": bool(out[2]),
             "queues_built": out[3]}
+
+
+def measure_reclaim_state():
+    """Measurement build only: the per-thread staging of exited threads
+    (engine.cpp Staging::hand_off / reclaim_drain) and the warm-up threads:
+    {handed_off, drained, busy (handed off with work in flight: 0),
+    warm_threads_started, warm_threads_done}."""
+    _need_measure()
+    out = (ctypes.c_long * 5)()
+    _current.leoec_measure_reclaim_state(out)
+    return {"handed_off": out[0], "drained": out[1], "busy": out[2],
+            "warm_threads_started": out[3], "warm_threads_done": out[4]}
 
 
 def measure_reset_knobs():

@@ -65,7 +65,6 @@ const Knobs* read_env() {
   k->host_pin = env_int("LEOEC_HOST_PIN", k->host_pin);
   k->host_pin_kib = env_int("LEOEC_HOST_PIN_KIB", k->host_pin_kib);
   k->zc_chunks = env_int("LEOEC_ZC_CHUNKS", k->zc_chunks);
-  k->zc_pin = env_int("LEOEC_ZC_PIN", k->zc_pin);
   k->large_chunks = env_int("LEOEC_LARGE_CHUNKS", k->large_chunks);
   k->host_batch = env_int("LEOEC_HOST_BATCH", k->host_batch);
   k->batch_window_us = env_int("LEOEC_BATCH_WINDOW_US", k->batch_window_us);

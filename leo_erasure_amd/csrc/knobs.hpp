@@ -30,14 +30,6 @@ struct Knobs {
                              //   pinning 140 MB per call costs more than the duplex gains
                              //   (100 MiB encode 2.67-2.86 ms one piece, 2.73-2.76 at 4 chunks,
                              //   3.08 at 8: profiles/r05_s29_ref_chunks*.log)
-  int zc_pin = 0;            // LEOEC_ZC_PIN=1 (measurement form): a per-thread zero-copy call
-                             //   pins the caller's blocks in place (hipHostRegister) and its
-                             //   kernel reads and writes them there instead of packing them into
-                             //   the thread's mapped buffer and unpacking the outputs
-                             //   (engine.cpp zc_in_place).  Not shipped: a lone 1 MiB call
-                             //   71.6-72.4 us against 71.2-81.6 packed, and 2-8 concurrent
-                             //   callers 15-18 GiB/s against 20-40 (registration serialises
-                             //   the callers; profiles/r05_s36_few_pin*.log, r05_s36_lone_pin*.log)
   int zc_chunks = 2;         // LEOEC_ZC_CHUNKS: a per-thread zero-copy call of a GF(2^w) map
                              //   in this many column chunks, packing chunk c + 1 while
                              //   chunk c's launch runs and unpacking each as it completes

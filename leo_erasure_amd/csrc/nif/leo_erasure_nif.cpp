@@ -271,7 +271,7 @@ int nif_load(ErlNifEnv*, void**, ERL_NIF_TERM) {
   if (devs.empty()) return 0;
   const int rc = leoec_host_spread(devs.data(), (int)devs.size());
   if (rc < 0 && leoec_host_lanes(nullptr, 0) > 0) {  // devices exist, the set is not theirs
-    std::fprintf(stderr, "leo_erasure: LEOEC_HOST_DEVICES=\"%s\": %s\n", spec,
+    std::fprintf(stderr, "leo_erasure: LEOEC_HOST_DEVICES=\"%s\": %s\n", spec ? spec : "(unset: all)",
                  leoec_strerror(rc));
     return 2;
   }

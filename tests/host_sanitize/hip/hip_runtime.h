@@ -185,6 +185,23 @@ inline int& fail_event_create_in() {
 }
 inline void fail_nth_event_create(int n) { fail_event_create_in() = n; }
 
+// Thread teardown: set on a thread once the first of its thread_local
+// destructors has started (tls_teardown.cpp re-registers the marker after
+// every thread_local destructor registration, so it runs before all of
+// them).  A HIP call from then on is what made rocprofv3 abort the bench's
+// host leg (profiles/r05_s6_bench_prof_host_leg_abort.txt: the tool's own
+// thread-local state may already be gone): every fake entry point aborts on it.
+inline bool& tls_teardown() {
+  static thread_local bool f = false;  // trivially destructible: no registration
+  return f;
+}
+inline void live(const char* fn) {
+  if (tls_teardown()) {
+    std::fprintf(stderr, "fake hip: %s called during thread-local teardown\n", fn);
+    std::abort();
+  }
+}
+
 inline std::atomic<long>& live_allocs() {
   static std::atomic<long> n{0};
   return n;
@@ -196,10 +213,12 @@ typedef fakehip::Stream* hipStream_t;
 typedef fakehip::Event* hipEvent_t;
 
 inline hipError_t hipGetDeviceCount(int* n) {
+  fakehip::live("hipGetDeviceCount");
   *n = fakehip::kDevices;
   return hipSuccess;
 }
 inline hipError_t hipGetDeviceProperties(hipDeviceProp_t* p, int dev) {
+  fakehip::live("hipGetDeviceProperties");
   if (dev < 0 || dev >= fakehip::kDevices) return hipErrorInvalidDevice;
   std::memset(p, 0, sizeof(*p));
   std::strcpy(p->name, "fake MI355X (host sanitizer harness)");
@@ -207,16 +226,19 @@ inline hipError_t hipGetDeviceProperties(hipDeviceProp_t* p, int dev) {
   return hipSuccess;
 }
 inline hipError_t hipSetDevice(int dev) {
+  fakehip::live("hipSetDevice");
   if (dev < 0 || dev >= fakehip::kDevices) return hipErrorInvalidDevice;
   fakehip::current_device() = dev;
   return hipSuccess;
 }
 inline hipError_t hipGetDevice(int* dev) {
+  fakehip::live("hipGetDevice");
   *dev = fakehip::current_device();
   return hipSuccess;
 }
 
 inline hipError_t hipMalloc(void** p, size_t n) {
+  fakehip::live("hipMalloc");
   *p = std::malloc(n ? n : 1);
   if (!*p) return hipErrorOutOfMemory;
   ++fakehip::live_allocs();
@@ -224,14 +246,17 @@ inline hipError_t hipMalloc(void** p, size_t n) {
 }
 template <class T>
 inline hipError_t hipMalloc(T** p, size_t n) {
+  fakehip::live("hipMalloc");
   return hipMalloc(reinterpret_cast<void**>(p), n);
 }
 inline hipError_t hipFree(void* p) {
+  fakehip::live("hipFree");
   if (p) --fakehip::live_allocs();
   std::free(p);
   return hipSuccess;
 }
 inline hipError_t hipHostMalloc(void** p, size_t n, unsigned) {
+  fakehip::live("hipHostMalloc");
   *p = std::malloc(n ? n : 1);
   if (!*p) return hipErrorOutOfMemory;
   ++fakehip::live_allocs();
@@ -240,6 +265,7 @@ inline hipError_t hipHostMalloc(void** p, size_t n, unsigned) {
   return hipSuccess;
 }
 inline hipError_t hipHostFree(void* p) {
+  fakehip::live("hipHostFree");
   if (p) {
     --fakehip::live_allocs();
     std::lock_guard<std::mutex> l(fakehip::pinned().mu);
@@ -249,6 +275,7 @@ inline hipError_t hipHostFree(void* p) {
   return hipSuccess;
 }
 inline hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned) {
+  fakehip::live("hipHostGetDevicePointer");
   // only pinned memory (hipHostMalloc, hipHostRegister) has a device address
   if (!fakehip::pinned().contains(h, 1)) {
     *d = nullptr;
@@ -259,22 +286,32 @@ inline hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned) {
 }
 
 inline hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned) {
+  fakehip::live("hipStreamCreateWithFlags");
   *s = new fakehip::Stream(fakehip::current_device());
   return hipSuccess;
 }
 inline hipError_t hipStreamDestroy(hipStream_t s) {
+  fakehip::live("hipStreamDestroy");
   delete s;
   return hipSuccess;
 }
 inline fakehip::Stream* fake_stream(hipStream_t s) { return s ? s : fakehip::null_stream(); }
 inline hipError_t hipStreamSynchronize(hipStream_t s) {
+  fakehip::live("hipStreamSynchronize");
   fakehip::Stream* st = fake_stream(s);
   st->wait(st->ticket());
   return hipSuccess;
 }
 
+inline hipError_t hipStreamQuery(hipStream_t s) {
+  fakehip::live("hipStreamQuery");
+  fakehip::Stream* st = fake_stream(s);
+  return st->reached(st->ticket()) ? hipSuccess : hipErrorNotReady;
+}
+
 inline hipError_t hipMemcpyAsync(void* dst, const void* src, size_t n, hipMemcpyKind kind,
                                  hipStream_t s) {
+  fakehip::live("hipMemcpyAsync");
   fakehip::Stream* st = fake_stream(s);
   const void* host = kind == hipMemcpyHostToDevice ? src : kind == hipMemcpyDeviceToHost ? dst
                                                                                           : nullptr;
@@ -292,6 +329,7 @@ inline hipError_t hipMemcpyAsync(void* dst, const void* src, size_t n, hipMemcpy
 // any pinned copy.  Overlapping an existing pinned block is refused, as the
 // runtime refuses it; unregistering under a copy in flight aborts the test.
 inline hipError_t hipHostRegister(void* p, size_t n, unsigned) {
+  fakehip::live("hipHostRegister");
   fakehip::Pinned& pn = fakehip::pinned();
   std::lock_guard<std::mutex> l(pn.mu);
   const uintptr_t a = (uintptr_t)p;
@@ -309,6 +347,7 @@ inline hipError_t hipHostRegister(void* p, size_t n, unsigned) {
   return hipSuccess;
 }
 inline hipError_t hipHostUnregister(void* p) {
+  fakehip::live("hipHostUnregister");
   fakehip::Pinned& pn = fakehip::pinned();
   std::lock_guard<std::mutex> l(pn.mu);
   auto it = pn.registered.find((uintptr_t)p);
@@ -324,6 +363,7 @@ inline hipError_t hipHostUnregister(void* p) {
 }
 
 inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) {
+  fakehip::live("hipEventCreateWithFlags");
   int& n = fakehip::fail_event_create_in();
   if (n > 0 && --n == 0) {
     *e = nullptr;
@@ -333,10 +373,12 @@ inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) {
   return hipSuccess;
 }
 inline hipError_t hipEventDestroy(hipEvent_t e) {
+  fakehip::live("hipEventDestroy");
   delete e;
   return hipSuccess;
 }
 inline hipError_t hipEventRecord(hipEvent_t e, hipStream_t s) {
+  fakehip::live("hipEventRecord");
   fakehip::Stream* st = fake_stream(s);
   std::lock_guard<std::mutex> l(e->mu);
   e->s = st;
@@ -344,6 +386,7 @@ inline hipError_t hipEventRecord(hipEvent_t e, hipStream_t s) {
   return hipSuccess;
 }
 inline hipError_t hipEventQuery(hipEvent_t e) {
+  fakehip::live("hipEventQuery");
   fakehip::Stream* st;
   uint64_t t;
   {
@@ -354,6 +397,7 @@ inline hipError_t hipEventQuery(hipEvent_t e) {
   return !st || st->reached(t) ? hipSuccess : hipErrorNotReady;
 }
 inline hipError_t hipEventSynchronize(hipEvent_t e) {
+  fakehip::live("hipEventSynchronize");
   fakehip::Stream* st;
   uint64_t t;
   {
@@ -368,6 +412,7 @@ inline hipError_t hipEventSynchronize(hipEvent_t e) {
 // Later work on s waits for what preceded e's record (on e's stream): the
 // wait is an operation of s's own thread, as the device's barrier packet.
 inline hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned) {
+  fakehip::live("hipStreamWaitEvent");
   fakehip::Stream* on;
   uint64_t t;
   {
@@ -381,4 +426,7 @@ inline hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned) {
 }
 
 inline const char* hipGetErrorString(hipError_t) { return "fake hip error"; }
-inline hipError_t hipGetLastError() { return hipSuccess; }
+inline hipError_t hipGetLastError() {
+  fakehip::live("hipGetLastError");
+  return hipSuccess;
+}

@@ -170,6 +170,12 @@ int main(int argc, char** argv) {
     if (!a.queue || !b.queue || b.pool_streams < 1 || b.pool_mapped < 1)
       fail("leoec_host_spread({0,1}) left a device without queue / pools");
     queues_after_warm = b.queues_built;
+    // both devices warmed by a thread of their own, which ended (its staging
+    // handed off while alive: no HIP call at its exit, tls_teardown.cpp)
+    const leoec::ReclaimState r = leoec::reclaim_state();
+    if (r.warm_threads_started != 2 || r.warm_threads_done != 2)
+      fail("warm threads started / done: " + std::to_string(r.warm_threads_started) + " / " +
+           std::to_string(r.warm_threads_done));
     if (queues_after_warm != 2) fail("queues built after warming 2 devices: " +
                                      std::to_string(queues_after_warm));
     if (leoec_host_spread(nullptr, 0) != 0) fail("leoec_host_spread reset (phase 0)");
@@ -200,7 +206,6 @@ int main(int argc, char** argv) {
         leoec_measure_set_knob("LEOEC_HOSTQ_STREAMS", (i / 7) % 2 ? "0" : "1");
         leoec_measure_set_knob("LEOEC_HOSTQ_SPLIT_KIB", i % 2 ? "0" : "1024");
         leoec_measure_set_knob("LEOEC_LARGE_CHUNKS", i % 3 == 0 ? "1" : i % 3 == 1 ? "8" : "3");
-        leoec_measure_set_knob("LEOEC_ZC_PIN", (i / 11) % 2 ? "0" : "1");
         ++i;
         std::this_thread::sleep_for(std::chrono::milliseconds(3));
       }
@@ -249,8 +254,7 @@ int main(int argc, char** argv) {
     Case d{LEOEC_VANDRS, 10, 4, 8, 262144};
     prepare(&d, 32);
     std::thread t([&] {
-      // the object 8 bytes past a 16-byte boundary: the in-place form
-      // (zc_in_place) declines it, so the call takes the packed column chunks
+      // (the object 8 bytes past a 16-byte boundary: packed column chunks)
       std::vector<uint8_t> shifted(c.size + 32);
       uint8_t* src = shifted.data() + ((24 - ((uintptr_t)shifted.data() & 15u)) & 15u);
       std::memcpy(src, c.data.data(), c.size);
@@ -355,6 +359,33 @@ int main(int argc, char** argv) {
     }
 #endif
     std::printf("large objects, pinned copies: %s\n", g_errs.empty() ? "ok" : "FAILED");
+  }
+
+  // phase 5: threads that come and go.  Each exiting caller thread hands its
+  // staging off with no HIP call (the fake runtime aborts on one from a
+  // thread_local destructor); a live thread's next call frees it.  Nothing a
+  // thread hands off may still be in flight (engine.cpp Reclaim invariant).
+  {
+    Case c{LEOEC_VANDRS, 10, 4, 8, 262144};
+    prepare(&c, 41);
+    const long before = leoec::reclaim_state().handed_off;
+    for (int wave = 0; wave < 4; ++wave) {
+      std::vector<std::thread> th;
+      for (int t = 0; t < 6; ++t)
+        th.emplace_back([&, t] {
+          if (t & 1) hipSetDevice(1);
+          roundtrip(c, wave + t, false);
+        });
+      for (auto& x : th) x.join();
+    }
+    roundtrip(c, 1, false);  // a live thread's call drains the list
+    const leoec::ReclaimState r = leoec::reclaim_state();
+    std::printf("thread exits: %ld stagings handed off (%ld this phase), %ld freed, %ld busy\n",
+                r.handed_off, r.handed_off - before, r.drained, r.busy);
+    if (r.handed_off - before < 24) fail("exited threads handed off fewer stagings than threads");
+    if (r.drained != r.handed_off) fail("handed-off stagings left undrained by a live call");
+    if (r.busy != 0) fail("a thread exited with work in flight or pins held");
+    std::printf("thread exits: %s\n", g_errs.empty() ? "ok" : "FAILED");
   }
 
   for (const auto& e : g_errs) std::fprintf(stderr, "ERROR %s\n", e.c_str());

@@ -570,17 +570,22 @@ import leo_erasure_amd as le
 from oracle import oracle as O
 torch.cuda.set_device(0)
 before = le._lib.measure_warm_state(0)
+free0, _ = torch.cuda.mem_get_info()
 t0 = time.perf_counter()
 n = le._lib.host_spread([0])
 t_spread = time.perf_counter() - t0
 after = le._lib.measure_warm_state(0)
+reclaim = le._lib.measure_reclaim_state()
 data = bytes(range(256)) * 4096 + b"tail"
 t0 = time.perf_counter()
 st, blocks = le.nif_encode("vandrs", (10, 4, 8), data, len(data))
 t_first = time.perf_counter() - t0
 final = le._lib.measure_warm_state(0)
 le._lib.host_spread([])
+torch.cuda.synchronize()
+free1, _ = torch.cuda.mem_get_info()
 print(json.dumps({"n": n, "before": before, "after": after, "final": final,
+                  "reclaim": reclaim, "leak_MiB": (free0 - free1) / 2**20,
                   "t_spread": t_spread, "t_first": t_first, "ok": st == "ok",
                   "parity": blocks == O.encode("vandrs", 10, 4, 8, data)}))
 """
@@ -591,7 +596,12 @@ def test_host_spread_warms_its_devices(gpu):
     gf_init warms the caller's device): in a fresh process that never called
     gf_init, host_spread([0]) builds device 0's batching queue and pools, and
     the first host call afterwards builds no queue and pays no start-up.
-    Child process on the measurement build (its warm-state counters)."""
+    The warm-up runs on a thread of its own even for a one-device set
+    (engine.cpp warm_devices), so this is the branch a multi-GPU node's NIF
+    load takes: the thread ran and ended, handed its staging back while alive
+    (its stream joined the pool), and the device memory the warm-up keeps is
+    bounded as in test_thread_exit_releases_staging.  Child process on the
+    measurement build (its warm-state and reclaim counters)."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     if not os.path.exists(os.path.join(root, "leo_erasure_amd", "libleoec_measure.so")):
         pytest.skip("measurement build absent (make -C leo_erasure_amd/csrc measure)")
@@ -604,6 +614,11 @@ def test_host_spread_warms_its_devices(gpu):
     assert not out["before"]["queue"] and out["before"]["queues_built"] == 0
     assert out["after"]["queue"] and out["after"]["queues_built"] == 1
     assert out["after"]["pool_streams"] >= 1 and out["after"]["pool_mapped"] >= 1
+    rc = out["reclaim"]
+    assert rc["warm_threads_started"] == 1 and rc["warm_threads_done"] == 1, rc
+    # the warm thread's own staging: handed off and freed before it ended
+    assert rc["handed_off"] == 1 and rc["drained"] == 1 and rc["busy"] == 0, rc
+    assert out["leak_MiB"] < 512, out
     assert out["final"]["queues_built"] == 1, "the first call after host_spread built a queue"
     assert out["ok"] and out["parity"]
     # a cold first call pays ~150-250 ms of runtime and queue set-up

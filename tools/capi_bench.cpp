@@ -18,6 +18,8 @@
 //   tools/capi_bench <libleoec*.so> mid      [K=V,...]   callers() from 4, 8, 16, 32 threads
 //   tools/capi_bench <libleoec*.so> sizes    [K=V,...]   callers() at 16 KiB - 4 MiB
 //                                                        objects, 8 and 32 threads
+//   tools/capi_bench <libleoec*.so> trace32  [K=V,...]   callers() from 32 threads,
+//                                                        encode then decode (copy trace)
 // K=V: measurement-build knobs (leoec_measure_set_knob), applied after load.
 #include <dlfcn.h>
 
@@ -328,6 +330,10 @@ int main(int argc, char** argv) {
     // where the per-thread path hands over to the batching queue
     for (bool dec : {false, true})
       for (int T : {4, 8, 16, 32}) callers(T, dec);
+  } else if (mode == "trace32") {
+    // the bench host leg's shape for a copy trace (rocprofv3 --kernel-trace
+    // --memory-copy-trace; tools/copy_gaps.py): 32 callers, encode then decode
+    for (bool dec : {false, true}) callers(32, dec);
   } else if (mode == "small") {
     // 16 KiB objects, 32 callers, encode (the queue's per-call cost)
     callers(32, false, 16ull << 10);

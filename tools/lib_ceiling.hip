@@ -19,7 +19,8 @@
 //            blocks' worth, no packet structure (the part's rate for this
 //            byte count)
 // on the reference geometry and on objects sized so packets are line
-// aligned (ps = 21,504 B), at 64 and 256 lanes per workgroup.
+// aligned (ps = 21,504 B), at 64 and 256 lanes per workgroup; then the
+// syndrome decode's access (dec_pattern: decode of data blocks {0,1}).
 //
 //   hipcc --offload-arch=gfx950 -O3 -o tools/lib_ceiling tools/lib_ceiling.hip
 //   tools/lib_ceiling [objects] [reps] [k]
@@ -203,6 +204,90 @@ sweep(const unsigned char* __restrict__ in, unsigned char* __restrict__ out, Geo
   }
 }
 
+// Decode {0,1} (round 6, verdict r5 item 5): the access of the syndrome
+// decode libb_dec_apply — one packet stream P (W packets), Q (W), then data
+// blocks 0..K-1, with data blocks 0 and 1 erased (their loads return zeros
+// through an empty buffer resource, no memory access) and LA packets in
+// flight — but the body only XORs: every packet into both output blocks'
+// packet x (no syndrome structure, no mask combine).  Inputs: the K - 2
+// surviving data blocks in the object row, P and Q in the parity buffer
+// (objects' 2 blocks each); outputs: data blocks 0 and 1 in the object row,
+// as the engine's device decode writes them.
+//   LA > 0  the shipped stream (zeros for the absent blocks)
+//   LA = 0  the block form: absent blocks skipped by a uniform branch, a
+//           present block's W loads in flight together
+//   PRESENT the ring over the present blocks only (P, Q, D2..): the stream
+//           the shipped kernel would have if its absent blocks cost nothing
+template <int K, int LA, int TW, bool PRESENT>
+__global__ void __launch_bounds__(TW) __attribute__((amdgpu_waves_per_eu(4, 8)))
+dec_pattern(unsigned char* __restrict__ rows, const unsigned char* __restrict__ par, Geo g) {
+  const unsigned b = obj_map(blockIdx.x, gridDim.x, g.tiles);
+  const unsigned obj = b / g.tiles, tile = b % g.tiles;
+  const unsigned off = tile * TW * 16u + threadIdx.x * 16u;
+  unsigned char* ib = rows + (size_t)obj * g.row;
+  const unsigned char* pb = par + (size_t)obj * 2 * g.bs;
+  // stream block s: 0 P, 1 Q, 2 + j data j (0, 1 erased: empty resource)
+  auto rs = [&](int s) {
+    if (s < 2) return rsrc(pb + (size_t)s * g.bs, g.bs);
+    return rsrc(ib + (size_t)(s - 2) * g.bs, s - 2 < 2 ? 0u : g.bs);
+  };
+  u4 A[W], B[W];
+  for (int x = 0; x < W; ++x) A[x] = B[x] = u4{0u, 0u, 0u, 0u};
+  auto eat = [&](int x, u4 v) {
+    A[x] ^= v;
+    B[x] ^= v;
+    pin(A[x]);
+    pin(B[x]);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  constexpr int NB = K + 2;
+  if constexpr (PRESENT) {
+    // present blocks: stream positions 0, 1, 4, 5, .. (P, Q, D2, ..)
+    constexpr int NPB = NB - 2, NP = NPB * W, RS = LA + 1;
+    auto blk = [](int i) { return i < 2 ? i : i + 2; };
+    u4 ring[RS];
+#pragma unroll
+    for (int q = 0; q < LA; ++q)
+      ring[q] = __builtin_amdgcn_raw_buffer_load_b128(rs(blk(q / W)), (unsigned)(q % W) * g.ps + off, 0, 2);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int q = p + LA;
+      if (q < NP)
+        ring[q % RS] = __builtin_amdgcn_raw_buffer_load_b128(rs(blk(q / W)), (unsigned)(q % W) * g.ps + off, 0, 2);
+      eat(p % W, ring[p % RS]);
+    }
+  } else if constexpr (LA == 0) {
+#pragma unroll
+    for (int s = 0; s < NB; ++s) {
+      if (s == 2 || s == 3) continue;  // the erased blocks: a uniform skip
+      const auto r = rs(s);
+      u4 y[W];
+#pragma unroll
+      for (int x = 0; x < W; ++x) y[x] = __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)x * g.ps + off, 0, 2);
+#pragma unroll
+      for (int x = 0; x < W; ++x) eat(x, y[x]);
+    }
+  } else {
+    constexpr int NP = NB * W, RS = LA + 1;
+    u4 ring[RS];
+#pragma unroll
+    for (int q = 0; q < LA; ++q)
+      ring[q] = __builtin_amdgcn_raw_buffer_load_b128(rs(q / W), (unsigned)(q % W) * g.ps + off, 0, 2);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int q = p + LA;
+      if (q < NP) ring[q % RS] = __builtin_amdgcn_raw_buffer_load_b128(rs(q / W), (unsigned)(q % W) * g.ps + off, 0, 2);
+      eat(p % W, ring[p % RS]);
+    }
+  }
+  if (off >= g.ps) return;
+#pragma unroll
+  for (int x = 0; x < W; ++x) {
+    __builtin_nontemporal_store(A[x], reinterpret_cast<u4*>(ib + (size_t)x * g.ps + off));
+    __builtin_nontemporal_store(B[x], reinterpret_cast<u4*>(ib + g.bs + (size_t)x * g.ps + off));
+  }
+}
+
 // A flat streaming kernel over the same bytes: lane l of tile t reads 16 B
 // at t * TW * 16 + l * 16 of each of the K data blocks (blocks as flat
 // rows, no packets) and writes the XOR to both output blocks.
@@ -362,6 +447,74 @@ int run(unsigned nobj, int reps) {
                                                  : "flat copy-xor wg256 (same bytes, no packets)";
     printf("{\"k\": %d, \"case\": \"%s\", \"ms_med\": %.4f, \"frac\": %.4f}\n", K, name.c_str(), ms,
            bytes / ms / 1e6 / 8000.0);
+  }
+  // decode {0,1}: the stream forms on the reference geometry, outputs (data
+  // blocks 0 and 1 of every object row) compared byte for byte; the parity
+  // buffer is `out` (its first 2 blocks per object), left as the encode
+  // forms wrote it
+  {
+    typedef void (*DFn)(unsigned char*, const unsigned char*, Geo);
+    struct DCase {
+      std::string name;
+      DFn k;
+      unsigned tw;
+    };
+#define DC(LA, TW, PR) reinterpret_cast<DFn>(&dec_pattern<K, LA, TW, PR>)
+    std::vector<DCase> dcases = {
+        {"decode {0,1}: stream la4 wg64 (shipped libb_dec_apply's access at k <= 4)", DC(4, 64, false), 64},
+        {"decode {0,1}: stream la2 wg64 (shipped at k >= 5, w <= 11)", DC(2, 64, false), 64},
+        {"decode {0,1}: block form wg64 (absent blocks skipped)", DC(0, 64, false), 64},
+        {"decode {0,1}: present blocks only, la4 wg64", DC(4, 64, true), 64},
+        {"decode {0,1}: present blocks only, la8 wg64", DC(8, 64, true), 64},
+        {"decode {0,1}: stream la4 wg256", DC(4, 256, false), 256},
+    };
+    Geo g = ref;
+    std::vector<unsigned char> a((size_t)nobj * g.row), b((size_t)nobj * g.row);
+    for (size_t c = 0; c < dcases.size(); ++c) {
+      g.tiles = (g.ps + dcases[c].tw * 16 - 1) / (dcases[c].tw * 16);
+      CHECK(hipMemset(in, 0, (size_t)nobj * g.row));  // D0, D1 rewritten, the rest zero
+      hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, (unsigned*)in, (size_t)nobj * g.row / 4, 9u);
+      hipLaunchKernelGGL(dcases[c].k, dim3(nobj * g.tiles), dim3(dcases[c].tw), 0, 0, in, out, g);
+      CHECK(hipMemcpy(c == 0 ? a.data() : b.data(), in, a.size(), hipMemcpyDeviceToHost));
+      if (c && a != b) {
+        printf("# decode form %s: output differs from the first decode form\n", dcases[c].name.c_str());
+        return 3;
+      }
+    }
+    printf("# every decode form wrote the same bytes\n");
+    std::vector<std::vector<float>> dt(dcases.size());
+    for (int round = 0; round < 4; ++round) {
+      for (size_t c = 0; c < dcases.size(); ++c) {
+        g.tiles = (g.ps + dcases[c].tw * 16 - 1) / (dcases[c].tw * 16);
+        const DFn kf = dcases[c].k;
+        const unsigned tw = dcases[c].tw;
+        auto launch = [=]() { hipLaunchKernelGGL(kf, dim3(nobj * g.tiles), dim3(tw), 0, 0, in, out, g); };
+        CHECK(hipEventRecord(e0, 0));
+        float ms = 0.f;
+        while (ms < 300.f) {
+          for (int i = 0; i < 10; ++i) launch();
+          CHECK(hipEventRecord(e1, 0));
+          CHECK(hipEventSynchronize(e1));
+          CHECK(hipEventElapsedTime(&ms, e0, e1));
+        }
+        for (int i = 0; i < reps; ++i) {
+          CHECK(hipEventRecord(e0, 0));
+          launch();
+          CHECK(hipEventRecord(e1, 0));
+          CHECK(hipEventSynchronize(e1));
+          CHECK(hipEventElapsedTime(&ms, e0, e1));
+          dt[c].push_back(ms);
+        }
+      }
+    }
+    CHECK(hipGetLastError());
+    for (size_t c = 0; c < dcases.size(); ++c) {
+      std::sort(dt[c].begin(), dt[c].end());
+      const double ms = dt[c][dt[c].size() / 2];
+      const double bytes = (double)nobj * (K + 2) * g.bs;  // K survivors in, 2 blocks out
+      printf("{\"k\": %d, \"case\": \"%s\", \"ms_med\": %.4f, \"frac\": %.4f}\n", K,
+             dcases[c].name.c_str(), ms, bytes / ms / 1e6 / 8000.0);
+    }
   }
   CHECK(hipFree(in));
   CHECK(hipFree(out));

@@ -27,7 +27,9 @@ def summarise(d, frag):
         for r in csv.DictReader(open(f)):
             if frag in r["Name"] and (best is None or int(r["Calls"]) > int(best["Calls"])):
                 best = r
-        if best:
+        # a 1-call match is a warm-up launch, not the launch the counters
+        # (the last dispatch) describe: no duration then
+        if best and int(best["Calls"]) > 1:
             out["avg_ns"] = float(best["AverageNs"])
             out["calls"] = int(best["Calls"])
             out["kernel"] = best["Name"]
