@@ -16,6 +16,7 @@
 // in launch order and wakes their callers.
 #include "hostq.hpp"
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -545,11 +546,14 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
     ticket->queue = q;
     return kNotBatched;
   }
+  // a batch's capacity (Knobs::hostq_slot_kib, at most the arenas); an empty
+  // slot takes any batchable job
+  const uint64_t cap = std::min<uint64_t>(kSlotBytes, (uint64_t)knobs().hostq_slot_kib << 10);
   Slot* s;
   for (;;) {
     s = q->open;
-    if (s && s->used_in + a_in <= kSlotBytes && s->used_out + a_out <= kSlotBytes &&
-        s->jobs.size() < kMaxJobs)
+    if (s && s->jobs.size() < kMaxJobs &&
+        (s->jobs.empty() || (s->used_in + a_in <= cap && s->used_out + a_out <= cap)))
       break;
     if (s) {  // full: hand it to the worker, open another
       s->state = St::kClosed;

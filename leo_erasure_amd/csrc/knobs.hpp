@@ -44,6 +44,9 @@ struct Knobs {
                              // the slot's stream (their cross-stream events cost more than the
                              // link's overlap gives: 16 / 64 KiB objects -5 % split,
                              // profiles/r05_s39_small_streams*.log)
+  int hostq_slot_kib = 16384;  // LEOEC_HOSTQ_SLOT_KIB: input (and output) bytes a batch may hold
+                             //   (at most the 16 MiB arenas; a lone job larger than this still
+                             //   takes an empty slot)
   int hostq_sync = 1;        // LEOEC_HOSTQ_SYNC: 1 poll events (hipEventQuery + yield),
                              //   0 hipEventSynchronize, 2 the same on blocking-sync events
   int hostq_close = 1;       // LEOEC_HOSTQ_CLOSE: 1 close a batch when the previous H2D is

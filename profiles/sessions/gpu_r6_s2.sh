@@ -18,4 +18,20 @@ TAILN=12 step r06_s2_lib_ceiling_k4 300 tools/lib_ceiling 1024 20 4
 TAILN=12 step r06_s2_lib_ceiling_k7 300 tools/lib_ceiling 1024 20 7
 TAILN=6 step r06_s2_ab_lib427_dec 300 python tools/env_ab.py --coding liberation --k 4 --m 2 --w 7 --objects 1024 --rounds 4 --erased 0,1 --variants ""
 TAILN=6 step r06_s2_ab_lib727_dec 300 python tools/env_ab.py --coding liberation --k 7 --m 2 --w 7 --objects 1024 --rounds 4 --erased 0,1 --variants ""
+# the batching queue's batch capacity and depth at 32 callers (item 3's A/B),
+# three rotated rounds, one process per run
+L=leo_erasure_amd/libleoec_measure.so
+V=("LEOEC_HOSTQ_SLOT_KIB=16384" "LEOEC_HOSTQ_SLOT_KIB=8192" "LEOEC_HOSTQ_SLOT_KIB=4096" "LEOEC_HOSTQ_SLOT_KIB=8192,LEOEC_HOSTQ_DEPTH=4" "LEOEC_HOSTQ_SLOT_KIB=4096,LEOEC_HOSTQ_DEPTH=4")
+for r in 0 1 2; do
+  for i in 0 1 2 3 4; do
+    v=${V[$(( (i + r) % 5 ))]}
+    n=$(echo $v | tr ',=' '__')
+    TAILN=2 step r06_s2_slot_${n}_$r 120 tools/capi_bench $L c32 $v
+  done
+done
+# cauchyrs(10,4,8) forms at more launch sizes (item 4)
+V2=";LEOEC_GFBIT_FORM=5,LEOEC_GFBIT_WG=64,LEOEC_GFBIT_PF=3;LEOEC_GFBIT_CBM=6"
+for n in 3072 8192; do
+  TAILN=9 step r06_s2_ab_cauchy_$n 300 python tools/env_ab.py --coding cauchyrs --k 10 --m 4 --w 8 --objects $n --rounds 3 --repair 0,5,10,13 --variants "$V2"
+done
 echo "session done"

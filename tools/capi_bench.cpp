@@ -330,6 +330,9 @@ int main(int argc, char** argv) {
     // where the per-thread path hands over to the batching queue
     for (bool dec : {false, true})
       for (int T : {4, 8, 16, 32}) callers(T, dec);
+  } else if (mode == "c32") {
+    // 32 callers, encode then decode (the bench host leg's concurrency; A/B)
+    for (bool dec : {false, true}) callers(32, dec);
   } else if (mode == "trace32") {
     // the bench host leg's shape for a copy trace (rocprofv3 --kernel-trace
     // --memory-copy-trace; tools/copy_gaps.py): 32 callers, encode then decode
