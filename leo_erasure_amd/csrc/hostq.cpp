@@ -598,7 +598,19 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
   // the worker waits for an open slot's FIRST reservation (or a closed
   // slot, or room on the GPU, notified where they happen)
   const bool wake = knobs().hostq_wake == 1;
-  if (!wake || s->reserved == 1) q->cv_worker.notify_one();
+  bool notify = !wake || s->reserved == 1;
+  if (knobs().hostq_eager && (s->used_in + a_in > cap || s->used_out + a_out > cap ||
+                              s->jobs.size() >= kMaxJobs)) {
+    // no room for another job of this size: the batch is complete, so it
+    // goes to the worker now, and its H2D queues behind the previous
+    // batch's instead of starting after it ends (tools/copy_gaps.py: at
+    // every gap of the H2D stream the previous batch alone was on the GPU)
+    s->state = St::kClosed;
+    q->closed.push_back(s);
+    q->open = nullptr;
+    notify = true;
+  }
+  if (notify) q->cv_worker.notify_one();
   lk.unlock();
 
   const bool gather = job.in.size() > 1;

@@ -47,6 +47,10 @@ struct Knobs {
   int hostq_slot_kib = 16384;  // LEOEC_HOSTQ_SLOT_KIB: input (and output) bytes a batch may hold
                              //   (at most the 16 MiB arenas; a lone job larger than this still
                              //   takes an empty slot)
+  int hostq_eager = 0;       // LEOEC_HOSTQ_EAGER=1: the caller whose reservation leaves no room for
+                             //   another job of its size hands the slot to the worker at once
+                             //   (0: the next caller finds it full, or the worker closes it when
+                             //   the previous batch's H2D ends, Knobs::hostq_close)
   int hostq_sync = 1;        // LEOEC_HOSTQ_SYNC: 1 poll events (hipEventQuery + yield),
                              //   0 hipEventSynchronize, 2 the same on blocking-sync events
   int hostq_close = 1;       // LEOEC_HOSTQ_CLOSE: 1 close a batch when the previous H2D is

@@ -205,6 +205,7 @@ int main(int argc, char** argv) {
         leoec_measure_set_knob("LEOEC_HOSTQ_WAKE", (i / 5) % 2 ? "0" : "1");
         leoec_measure_set_knob("LEOEC_HOSTQ_STREAMS", (i / 7) % 2 ? "0" : "1");
         leoec_measure_set_knob("LEOEC_HOSTQ_SPLIT_KIB", i % 2 ? "0" : "1024");
+        leoec_measure_set_knob("LEOEC_HOSTQ_EAGER", (i / 2) % 2 ? "1" : "0");
         leoec_measure_set_knob("LEOEC_HOSTQ_SLOT_KIB", i % 3 == 0 ? "16384" : i % 3 == 1 ? "4096" : "512");
         leoec_measure_set_knob("LEOEC_LARGE_CHUNKS", i % 3 == 0 ? "1" : i % 3 == 1 ? "8" : "3");
         ++i;

@@ -23,7 +23,7 @@
 // syndrome decode's access (dec_pattern: decode of data blocks {0,1}).
 //
 //   hipcc --offload-arch=gfx950 -O3 -o tools/lib_ceiling tools/lib_ceiling.hip
-//   tools/lib_ceiling [objects] [reps] [k]
+//   tools/lib_ceiling [objects] [reps] [k] [decode-form]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -327,8 +327,10 @@ struct Case {
   unsigned st = 0;  // sweep form: tiles per wave (grid = objects x ceil(tiles / st))
 };
 
+// only >= 0: launch decode form `only` `reps` times and nothing else (a
+// target for rocprofv3 --pmc passes: tools/pmc_r6_libdec.sh)
 template <int K>
-int run(unsigned nobj, int reps) {
+int run(unsigned nobj, int reps, int only) {
   // liberation geometry (engine op_layout): bs = ceil16(ceil(N / (k w))) * w
   auto geo = [&](unsigned long long osz) {
     Geo g{};
@@ -374,7 +376,7 @@ int run(unsigned nobj, int reps) {
   };
   // every packet form computes the same XORs: outputs compared with the
   // first form's, byte for byte, on the reference geometry
-  {
+  if (only < 0) {
     std::vector<unsigned char> a(out_bytes), b(out_bytes);
     for (size_t c = 0; c < cases.size(); ++c) {
       if (cases[c].aligned) continue;
@@ -396,7 +398,7 @@ int run(unsigned nobj, int reps) {
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   std::vector<std::vector<float>> t(cases.size() + 2);
-  for (int round = 0; round < 4; ++round) {
+  for (int round = 0; round < (only < 0 ? 4 : 0); ++round) {
     for (size_t c = 0; c < cases.size() + 2; ++c) {
       Geo g = c < cases.size() && cases[c].aligned ? ali : ref;
       std::function<void()> launch;
@@ -437,7 +439,7 @@ int run(unsigned nobj, int reps) {
     }
   }
   CHECK(hipGetLastError());
-  for (size_t c = 0; c < cases.size() + 2; ++c) {
+  for (size_t c = 0; only < 0 && c < cases.size() + 2; ++c) {
     std::sort(t[c].begin(), t[c].end());
     const double ms = t[c][t[c].size() / 2];
     const Geo g = c < cases.size() && cases[c].aligned ? ali : ref;
@@ -469,6 +471,15 @@ int run(unsigned nobj, int reps) {
         {"decode {0,1}: stream la4 wg256", DC(4, 256, false), 256},
     };
     Geo g = ref;
+    if (only >= 0) {
+      if (only >= (int)dcases.size()) return 4;
+      g.tiles = (g.ps + dcases[only].tw * 16 - 1) / (dcases[only].tw * 16);
+      for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL(dcases[only].k, dim3(nobj * g.tiles), dim3(dcases[only].tw), 0, 0, in, out, g);
+      CHECK(hipDeviceSynchronize());
+      printf("# decode form %s: %d launches\n", dcases[only].name.c_str(), reps);
+      return 0;
+    }
     std::vector<unsigned char> a((size_t)nobj * g.row), b((size_t)nobj * g.row);
     for (size_t c = 0; c < dcases.size(); ++c) {
       g.tiles = (g.ps + dcases[c].tw * 16 - 1) / (dcases[c].tw * 16);
@@ -526,6 +537,7 @@ int main(int argc, char** argv) {
   const unsigned nobj = argc > 1 ? (unsigned)atoi(argv[1]) : 1024u;
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
   const int k = argc > 3 ? atoi(argv[3]) : 7;
-  if (k == 4) return run<4>(nobj, reps);
-  return run<7>(nobj, reps);
+  const int only = argc > 4 ? atoi(argv[4]) : -1;  // a decode form alone (PMC target)
+  if (k == 4) return run<4>(nobj, reps, only);
+  return run<7>(nobj, reps, only);
 }

@@ -4,7 +4,7 @@
     python tools/rocprof_summary.py gpurun_out/prof > profiles/<name>.txt
     python tools/rocprof_summary.py --by-launch gpurun_out/prof   # per (kernel, grid, VGPRs)
 
---by-launch (rocpd .db only) splits a kernel's launches by grid size, so one
+--by-launch (rocpd .db, or a kernel_trace.csv) splits a kernel's launches by grid size, so one
 kernel run over several configs (objects x block sizes) reads per config.
 """
 import csv
@@ -24,11 +24,15 @@ def from_db(path, by_launch=False):
             for r in c.execute(q)]
 
 
-def from_trace_csv(path):
+def from_trace_csv(path, by_launch=False):
     rows = []
     with open(path) as fh:
         for r in csv.DictReader(fh):
-            rows.append((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+            name = r["Kernel_Name"]
+            if by_launch:
+                vg = int(r.get("VGPR_Count") or 0) + int(r.get("Accum_VGPR_Count") or 0)
+                name = f"{name[:110]} | grid {r['Grid_Size_X']} wg {r['Workgroup_Size_X']} vgpr {vg}"
+            rows.append((name, int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
     return rows
 
 
@@ -37,7 +41,7 @@ def main(d, by_launch=False):
     for p in glob.glob(os.path.join(d, "**", "*.db"), recursive=True):
         rows += from_db(p, by_launch)
     for p in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
-        rows += from_trace_csv(p)
+        rows += from_trace_csv(p, by_launch)
     stats = defaultdict(list)
     for name, s, e in rows:
         stats[name].append(e - s)
