@@ -2,10 +2,12 @@
 // (cauchyrs; kernels_impl.hpp gfbit_apply for the arithmetic), R <= 4
 // outputs per launch, inputs beyond 16 folded in by accumulating launches.
 //
-// gfbit_apply (kernels_impl.hpp) is shipped; this TU holds its launch
-// dispatch only.  The measurement forms (gfb2_apply, gfbx_apply,
-// gfba_apply, the lane-width / look-ahead / register-cap / LDS variants)
-// live in gfbit_measure.hip, compiled into the measurement library only.
+// gfbit_apply (kernels_impl.hpp) is shipped, and gfbk_apply (gfbit_impl.hpp)
+// for launches of at least kGfbkMinBytes of the (w = 8, K = 10, 4 rows)
+// shape; this TU holds their launch dispatch (and gfbk's instance).  The
+// measurement forms (gfb2_apply, gfbx_apply, gfba_apply, the lane-width /
+// look-ahead / register-cap / LDS variants) live in gfbit_measure.hip,
+// compiled into the measurement library only.
 #include <utility>
 
 #include "gfbit_impl.hpp"
@@ -18,14 +20,14 @@ namespace {
 
 using namespace gfbit_detail;
 
-GfbFn pick(const GfBitApply& p, int w, int r, bool acc, int nk) {
+GfbFn pick(const GfBitApply& p, int w, int r, bool acc, int nk, uint64_t no) {
+  // large cauchyrs(k = 10, w = 8)-shaped launches: gfbk_apply (gfbit_impl.hpp)
+  const bool big = gfbk_pays(p, r, acc, nk, no);
 #ifdef LEOEC_MEASURE
   // the measurement forms (gfbit_measure.hip) where LEOEC_GFBIT_* selects one
-  if (GfbFn f = pick_measure(p, w, r, acc, nk)) return f;
-#else
-  (void)p;
-  (void)nk;
+  if (GfbFn f = pick_measure(p, w, r, acc, nk, big)) return f;
 #endif
+  if (big) return &launch_gfbk_t<3, 64, false, 1>;
   switch (w) {
     case 8: return shipped<8>(r, acc);
     case 2: return shipped<2>(r, acc);
@@ -76,7 +78,7 @@ int launch(const GfBitApply& p, hipStream_t s) {
       const int nr = (p.R - r0 < kMaxR) ? p.R - r0 : kMaxR;
       for (int j0 = 0; j0 < p.K; j0 += kMaxK) {
         const int nk = (p.K - j0 < kMaxK) ? p.K - j0 : kMaxK;
-        const int rc = pick(p, w, nr, j0 > 0, nk)(p, r0, j0, nk, o0, no, s);
+        const int rc = pick(p, w, nr, j0 > 0, nk, no)(p, r0, j0, nk, o0, no, s);
         if (rc) return rc;
       }
     }

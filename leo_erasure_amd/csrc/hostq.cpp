@@ -109,6 +109,7 @@ struct Queue {
   Slot slots[kSlots];
   Slot* open = nullptr;
   std::deque<Slot*> closed;    // closed by a caller because it was full
+  std::atomic<int> nclosed{0}; // closed.size(), read without the lock (wait_h2d_or_closed)
   std::deque<Slot*> inflight;  // launch order
   Slot* last = nullptr;        // most recently launched
   int direct = 0;              // calls on their per-thread path (HostqTicket)
@@ -128,6 +129,22 @@ hipError_t wait_event(hipEvent_t ev) {
     }
   }
   return hipEventSynchronize(ev);
+}
+
+// The worker's wait for the previous batch's input copy (Knobs::hostq_close =
+// 1), cut short when a caller hands over a complete batch meanwhile (it can
+// be issued at once: its H2D queues behind the running one).  True when the
+// copy is done.
+bool wait_h2d_or_closed(hipEvent_t ev, const Queue* q) {
+  if (knobs().hostq_sync != 1) {
+    (void)wait_event(ev);  // (a failed copy is the batch's status: the completer reports it)
+    return true;
+  }
+  for (;;) {
+    if (hipEventQuery(ev) != hipErrorNotReady) return true;
+    if (q->nclosed.load(std::memory_order_acquire) > 0) return false;
+    std::this_thread::yield();
+  }
 }
 
 int slot_alloc(Slot* s) {
@@ -273,15 +290,16 @@ void worker_main(Queue* q) {
         q->last->state == St::kInflight) {
       Slot* prev = q->last;
       lk.unlock();
-      (void)wait_event(prev->ev_h2d);
+      const bool copied = wait_h2d_or_closed(prev->ev_h2d, q);
       lk.lock();
-      q->last = nullptr;
+      if (copied && q->last == prev) q->last = nullptr;
       continue;
     }
     Slot* s;
     if (!q->closed.empty()) {
       s = q->closed.front();
       q->closed.pop_front();
+      q->nclosed.fetch_sub(1, std::memory_order_release);
     } else {
       s = q->open;
       // measurement knob: hold an idle-GPU batch open for a window
@@ -558,6 +576,7 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
     if (s) {  // full: hand it to the worker, open another
       s->state = St::kClosed;
       q->closed.push_back(s);
+      q->nclosed.fetch_add(1, std::memory_order_release);
       q->open = nullptr;
       q->cv_worker.notify_one();
     }
@@ -607,6 +626,7 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
     // every gap of the H2D stream the previous batch alone was on the GPU)
     s->state = St::kClosed;
     q->closed.push_back(s);
+    q->nclosed.fetch_add(1, std::memory_order_release);
     q->open = nullptr;
     notify = true;
   }

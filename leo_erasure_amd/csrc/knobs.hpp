@@ -117,6 +117,9 @@ struct Knobs {
   int gfbit_cbm = 0;         // LEOEC_GFBIT_CBM: cauchyrs(10,4,8) encode with its bitmatrix compiled
                              //   in (cbm_inst.hip): 0 off, 1 64 lanes 2 waves 16 packets in flight, 2 the same
                              //   with 10, 3 128 lanes, 4 64 lanes 3 waves 4 in flight, 5 256 lanes
+  int gfbk_min_mib = -1;     // LEOEC_GFBK_MIN_MIB: launches of at least this many MiB of algorithmic
+                             //   bytes take gfbk_apply (w = 8, K = 10, 4 rows; -1: the shipped
+                             //   kGfbkMinBytes, gfbit_impl.hpp; a huge value: never)
   int gfbit_form = 0;        // LEOEC_GFBIT_FORM: 0 gfbit_apply (shipped), 1 gfb2_apply (buffer loads)
 };
 

@@ -320,6 +320,46 @@ def test_baseline_configs_1MiB_device_batches(gpu, le, oracle, cls, k, m, w):
         assert gpu.equal(out[r], blocks[b]), (cls, b)
 
 
+@pytest.mark.parametrize("n,size", [(2800, 1048576), (2720, 1048576 + 77)])
+def test_cauchy_large_launch_gfbk(gpu, le, oracle, n, size):
+    """cauchyrs(10,4,8) launches of at least kGfbkMinBytes (4.0 GB of
+    algorithmic bytes) take gfbk_apply (gfbit_impl.hpp, round 6): 2,800 x
+    1 MiB (4.11 GB) takes it for encode, decode of 4 data blocks and repair
+    of 4 blocks; 2,720 ragged objects (3.99 GB) stay on gfbit_apply.  Encode
+    parity against the oracle for objects at both ends and in the middle;
+    decode over poisoned blocks back to the objects; repair against the
+    encoded blocks."""
+    k, m, w, cls = 10, 4, 8, "cauchyrs"
+    bs, _ = le.layout(cls, (k, m, w), size)
+    stride = (size + 15) // 16 * 16
+    g = gpu.Generator(device="cuda")
+    g.manual_seed(0x6FB4 + n)
+    objs = gpu.randint(0, 256, (n, stride), dtype=gpu.uint8, device="cuda", generator=g)
+    parity = gpu.full((n, m * bs), 0x5A, dtype=gpu.uint8, device="cuda")
+    le.device.encode(cls, (k, m, w), objs, size, parity)
+    gpu.cuda.synchronize()
+    for o in (0, 1, n // 2, n - 2, n - 1):
+        ref = oracle.encode(cls, k, m, w, objs[o, :size].cpu().numpy().tobytes())
+        assert parity[o].cpu().numpy().tobytes() == b"".join(ref[k:]), f"object {o}"
+    ref = objs.clone()
+    objs[:, :m * bs] = 0xA5
+    le.device.decode(cls, (k, m, w), objs, size, parity, list(range(m)))
+    gpu.cuda.synchronize()
+    assert gpu.equal(objs[:, :size], ref[:, :size])
+    del ref
+    pad = gpu.zeros((n, k * bs), dtype=gpu.uint8, device="cuda")
+    pad[:, :size] = objs[:, :size]
+    lost = [0, 5, 10, 13]
+    blocks = [pad[:, b * bs:(b + 1) * bs] if b < k else parity[:, (b - k) * bs:(b - k + 1) * bs]
+              for b in range(k + m)]
+    avail = [None if b in lost else blocks[b].contiguous() for b in range(k + m)]
+    out = [gpu.full((n, bs), 0x3C, dtype=gpu.uint8, device="cuda") for _ in lost]
+    le.device.repair(cls, (k, m, w), avail, bs, lost, out, n)
+    gpu.cuda.synchronize()
+    for r, b in enumerate(lost):
+        assert gpu.equal(out[r], blocks[b]), b
+
+
 def test_golden_fixtures_gpu(gpu, le):
     """The committed restatement-derived fixtures, through the GPU engine."""
     import json
