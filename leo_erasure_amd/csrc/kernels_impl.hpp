@@ -730,6 +730,8 @@ struct LibDecArgs {
   uint32_t tiles;
   uint32_t vmin;          // min valid over every shard read or written
   uint32_t xmap;          // 1: xcd_obj_map
+  uint32_t combine;       // libb_dec_apply's D_E = B_CE^-1 S_C: 0 a masked XOR per (syndrome,
+                          // packet), 1 an XOR only where the bit is set (uniform branches)
 };
 
 constexpr int lib_dec_waves(int w) { return w <= 5 ? 4 : w <= 11 ? 3 : 2; }
@@ -999,15 +1001,25 @@ __device__ __forceinline__ void libb_dec_tile(const LibDecArgs& a, uint64_t o64,
     u32x4 acc[W];
 #pragma unroll
     for (int x = 0; x < W; ++x) acc[x] = u32x4{0u, 0u, 0u, 0u};
+    if (a.combine == 1u) {  // wave-uniform: XOR only the set bits
 #pragma unroll
-    for (int s = 0; s < 2 * W; ++s) {
-      const uint32_t bits = a.mbits[b][s];  // wave-uniform
-      if (bits != 0u) {
+      for (int s = 0; s < 2 * W; ++s) {
+        const uint32_t bits = a.mbits[b][s];  // wave-uniform
 #pragma unroll
-        for (int x = 0; x < W; ++x) {
-          const uint32_t m = (uint32_t)((int32_t)(bits << x) >> 31);
+        for (int x = 0; x < W; ++x)
+          if ((bits << x) & 0x80000000u) acc[x] ^= S[s];
+      }
+    } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[x][e] ^= S[s][e] & m;
+      for (int s = 0; s < 2 * W; ++s) {
+        const uint32_t bits = a.mbits[b][s];  // wave-uniform
+        if (bits != 0u) {
+#pragma unroll
+          for (int x = 0; x < W; ++x) {
+            const uint32_t m = (uint32_t)((int32_t)(bits << x) >> 31);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[x][e] ^= S[s][e] & m;
+          }
         }
       }
     }

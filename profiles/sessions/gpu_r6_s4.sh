@@ -28,4 +28,10 @@ V2=";LEOEC_GFBK_MIN_MIB=99999999"
 for n in 2048 2560 2816 3072; do
   TAILN=6 step r06_s4_ab_gfbk_$n 300 python tools/env_ab.py --coding cauchyrs --k 10 --m 4 --w 8 --objects $n --rounds 4 --repair 0,5,10,13 --variants "$V2"
 done
+# liberation syndrome decode: masked vs set-bit combine (item 5's counters:
+# the kernel issues 3.2x the pattern's VALU instructions, memory identical)
+V3=";LEOEC_LIB_DEC_COMBINE=1"
+TAILN=6 step r06_s4_ab_lib427_combine 300 python tools/env_ab.py --coding liberation --k 4 --m 2 --w 7 --objects 1024 --rounds 4 --erased 0,1 --variants "$V3"
+TAILN=6 step r06_s4_ab_lib727_combine 300 python tools/env_ab.py --coding liberation --k 7 --m 2 --w 7 --objects 1024 --rounds 4 --erased 0,1 --repair 0,7 --variants "$V3"
+TAILN=6 step r06_s4_ab_lib10211_combine 300 python tools/env_ab.py --coding liberation --k 10 --m 2 --w 11 --objects 1024 --rounds 4 --erased 0,1 --variants "$V3"
 echo "session done"
