@@ -538,12 +538,6 @@ struct Staging {
   uint8_t* zd = nullptr;    //   the same memory's device address
   size_t zcap = 0;
   bool zc = false;          // this call's device pointers are in [zd, zd + zcap)
-  std::vector<uintptr_t> pins;  // registrations this call uses (pin_acquire), released
-                                // once its copies are done (pins_release)
-  hipStream_t up = nullptr;     // large_chunked: the H2D copies
-  hipStream_t down = nullptr;   //   and the D2H copies, beside `stream`'s launches
-  hipEvent_t ev_in[kStageSlots] = {};  // large_chunked: chunk c's H2D done
-  hipEvent_t ev_k[kStageSlots] = {};   //   chunk c's launch done
 
   Staging() = default;
   Staging(const Staging&) = delete;
@@ -562,21 +556,19 @@ struct Staging {
 
 // Invariant: a per-thread call leaves nothing of itself in flight when it
 // returns — stage_d2h_sync, zc_chunked and every error path synchronise the
-// thread's stream (large_chunked also its two copy streams) and release its
-// pins — so a thread's staging is idle whenever the thread can exit, and
+// thread's stream — so a thread's staging is idle whenever the thread can exit, and
 // its handles can be freed by any other thread.  reclaim_drain checks it
 // (hipStreamQuery on each handed-off stream; a busy one is counted in
 // ReclaimState::busy and synchronised before reuse) and the sanitizer harness
 // asserts the count is zero (tests/host_sanitize/host_stress.cpp).
 struct Reclaim {
   int device = -1;
-  hipStream_t streams[3] = {};
+  hipStream_t stream = nullptr;
   std::vector<hipEvent_t> events;
   uint8_t* buf = nullptr;   // hipMalloc
   uint8_t* ring = nullptr;  // hipHostMalloc
   uint8_t* hbuf = nullptr;  // hipHostMalloc
   ResourcePool::Mapped mapped{nullptr, nullptr, 0};
-  size_t npins = 0;         // registrations still held (must be 0)
 };
 // Heap-allocated and never freed, as g_pool: a thread may exit while exit()
 // runs the static destructors.
@@ -589,17 +581,13 @@ void Staging::hand_off() {
   if (device >= 0 && stream) {
     Reclaim r;
     r.device = device;
-    r.streams[0] = stream;
-    r.streams[1] = up;
-    r.streams[2] = down;
-    for (hipEvent_t* set : {ev, ev_in, ev_k})
-      for (int i = 0; i < kStageSlots; ++i)
-        if (set[i]) r.events.push_back(set[i]);
+    r.stream = stream;
+    for (hipEvent_t e : ev)
+      if (e) r.events.push_back(e);
     r.buf = buf;
     r.ring = ring;
     r.hbuf = hbuf;
     if (zh) r.mapped = ResourcePool::Mapped{zh, zd, zcap};
-    r.npins = pins.size();
     {
       std::lock_guard<std::mutex> l(*g_reclaim_mu);
       g_reclaim->push_back(std::move(r));
@@ -608,13 +596,11 @@ void Staging::hand_off() {
     g_reclaim_pending.fetch_add(1, std::memory_order_release);
   }
   device = -1;
-  stream = up = down = nullptr;
-  for (hipEvent_t* set : {ev, ev_in, ev_k})
-    for (int i = 0; i < kStageSlots; ++i) set[i] = nullptr;
+  stream = nullptr;
+  for (hipEvent_t& e : ev) e = nullptr;
   buf = ring = hbuf = zh = zd = nullptr;
   cap = chunk = hcap = zcap = 0;
   zc = false;
-  pins.clear();
   for (bool& b : busy) b = false;
   next = 0;
 }
@@ -633,14 +619,11 @@ void reclaim_drain() {
   }
   for (Reclaim& r : todo) {
     DeviceScope on(r.device);
-    bool busy = r.npins != 0;
-    for (hipStream_t s : r.streams)
-      if (s && hipStreamQuery(s) != hipSuccess) {
-        (void)hipGetLastError();  // (not-ready is not an error of any call)
-        busy = true;
-        (void)hipStreamSynchronize(s);
-      }
-    if (busy) g_reclaim_busy.fetch_add(1, std::memory_order_relaxed);
+    if (hipStreamQuery(r.stream) != hipSuccess) {
+      (void)hipGetLastError();  // (not-ready is not an error of any call)
+      g_reclaim_busy.fetch_add(1, std::memory_order_relaxed);
+      (void)hipStreamSynchronize(r.stream);
+    }
     for (hipEvent_t e : r.events) (void)hipEventDestroy(e);
     if (r.buf) (void)hipFree(r.buf);
     if (r.ring) (void)hipHostFree(r.ring);
@@ -649,8 +632,7 @@ void reclaim_drain() {
     bool pooled = false;
     {
       std::lock_guard<std::mutex> l(p.mu);
-      for (hipStream_t s : r.streams)
-        if (s) p.streams.push_back(s);
+      p.streams.push_back(r.stream);
       if (r.mapped.h && r.mapped.cap <= kPoolMapped) {
         p.mapped.push_back(r.mapped);
         pooled = true;
@@ -801,119 +783,11 @@ bool ring_ready(Staging* st) {
   return true;
 }
 
-#ifdef LEOEC_MEASURE  // (measurement build only)
-// Caller memory pinned in place for the copies of one large call
-// (Knobs::host_pin).  Pages are pinned with hipHostRegister in page-aligned,
-// non-overlapping registrations with a user count: a call pins the gaps of
-// its range that no registration covers yet and joins the ones that do
-// (decode survivors are often sub-binaries of one parent binary, sharing
-// pages at their edges; concurrent calls on one binary share its
-// registrations), and a registration is released when its last user's
-// copies are done.  Copies are cut at registration edges, so each lies in
-// one registration.  A range the runtime refuses to pin (the host
-// application registered it itself) is copied as pageable memory, which the
-// runtime stages through its own buffers.
-struct PinnedRange {
-  uintptr_t hi;
-  int users;
-};
-std::mutex g_pin_mu;
-std::map<uintptr_t, PinnedRange> g_pins;  // lo -> range
-constexpr uintptr_t kPage = 4096;
-constexpr size_t kPinMin = (size_t)1 << 20;
-
-// Pins [p, p + n); on success appends the registration edges inside the
-// range to `cuts` (ascending) and the registrations used to st->pins.
-bool pin_acquire(Staging* st, const void* p, size_t n, std::vector<uintptr_t>* cuts) {
-  const uintptr_t lo = (uintptr_t)p & ~(kPage - 1);
-  const uintptr_t hi = ((uintptr_t)p + n + kPage - 1) & ~(kPage - 1);
-  std::lock_guard<std::mutex> l(g_pin_mu);
-  std::vector<std::pair<uintptr_t, uintptr_t>> gaps;
-  std::vector<uintptr_t> joined;
-  auto it = g_pins.upper_bound(lo);
-  if (it != g_pins.begin() && std::prev(it)->second.hi > lo) --it;
-  uintptr_t cur = lo;
-  for (; it != g_pins.end() && it->first < hi; ++it) {
-    if (it->first > cur) gaps.emplace_back(cur, it->first);
-    joined.push_back(it->first);
-    cur = std::max(cur, it->second.hi);
-  }
-  if (cur < hi) gaps.emplace_back(cur, hi);
-  for (size_t g = 0; g < gaps.size(); ++g) {
-    if (hipHostRegister(reinterpret_cast<void*>(gaps[g].first), gaps[g].second - gaps[g].first,
-                        hipHostRegisterPortable) != hipSuccess) {
-      (void)hipGetLastError();
-      for (size_t u = 0; u < g; ++u) (void)hipHostUnregister(reinterpret_cast<void*>(gaps[u].first));
-      return false;
-    }
-  }
-  for (const auto& g : gaps) {
-    g_pins[g.first] = PinnedRange{g.second, 1};
-    st->pins.push_back(g.first);
-  }
-  for (uintptr_t j : joined) {
-    ++g_pins[j].users;
-    st->pins.push_back(j);
-  }
-  for (auto r = g_pins.upper_bound((uintptr_t)p); r != g_pins.end() && r->first < (uintptr_t)p + n;
-       ++r)
-    cuts->push_back(r->first);
-  return true;
-}
-
-// After the call's copies have completed (its stream synchronised).
-void pins_release(Staging* st) {
-  if (st->pins.empty()) return;
-  std::lock_guard<std::mutex> l(g_pin_mu);
-  for (uintptr_t lo : st->pins) {
-    auto it = g_pins.find(lo);
-    if (it != g_pins.end() && --it->second.users == 0) {
-      (void)hipHostUnregister(reinterpret_cast<void*>(lo));
-      g_pins.erase(it);
-    }
-  }
-  st->pins.clear();
-}
-#else
-// The product build never pins caller memory (Knobs::host_pin = 0,
-// Knobs::large_chunks = 1): no registration is ever held.
-void pins_release(Staging* st) { st->pins.clear(); }
-#endif  // LEOEC_MEASURE
-
-// One host <-> device copy of a large segment on st->stream: from pinned
-// caller memory in pieces of at most Knobs::host_pin_kib (0: no bound), cut
-// at registration edges; else one pageable copy.
-int copy_large(Staging* st, void* dst, const void* src, size_t n, hipMemcpyKind kind) {
-  const bool h2d = kind == hipMemcpyHostToDevice;
-  const uint8_t* host = static_cast<const uint8_t*>(h2d ? src : dst);
-#ifdef LEOEC_MEASURE
-  std::vector<uintptr_t> cuts;
-  if (knobs().host_pin && n >= kPinMin && pin_acquire(st, host, n, &cuts)) {
-    const size_t piece = knobs().host_pin_kib > 0 ? (size_t)knobs().host_pin_kib << 10 : n;
-    cuts.push_back((uintptr_t)host + n);
-    size_t off = 0;
-    for (uintptr_t edge : cuts) {
-      const size_t stop = (size_t)(edge - (uintptr_t)host);
-      for (; off < stop; off += std::min(piece, stop - off)) {
-        const size_t len = std::min(piece, stop - off);
-        if (hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, static_cast<const uint8_t*>(src) + off,
-                           len, kind, st->stream) != hipSuccess)
-          return LEOEC_E_HIP;
-      }
-    }
-    return LEOEC_OK;
-  }
-#else
-  (void)host;
-#endif
-  return hip_ok(hipMemcpyAsync(dst, src, n, kind, st->stream));
-}
-
 // Host -> device, ordered on st->stream; returns once `src` may be reused
-// (a pinned source: once the stream is synchronised, before pins_release).
+// (a pageable copy is staged by the runtime before it returns).
 int stage_h2d(Staging* st, uint8_t* dev, const uint8_t* src, size_t n) {
   if (n == 0) return LEOEC_OK;
-  if (!ring_ready(st)) return copy_large(st, dev, src, n, hipMemcpyHostToDevice);
+  if (!ring_ready(st)) return hip_ok(hipMemcpyAsync(dev, src, n, hipMemcpyHostToDevice, st->stream));
   for (size_t off = 0; off < n; off += st->chunk) {
     const size_t len = std::min(st->chunk, n - off);
     const int s = st->next;
@@ -982,9 +856,9 @@ int stage_d2h_sync_impl(Staging* st, const std::vector<D2HSeg>& segs) {
   if (!ring_ready(st)) {
     int rc = LEOEC_OK;
     for (const D2HSeg& g : segs)
-      if (g.n && (rc = copy_large(st, g.host, g.dev, g.n, hipMemcpyDeviceToHost))) break;
+      if (g.n && (rc = hip_ok(hipMemcpyAsync(g.host, g.dev, g.n, hipMemcpyDeviceToHost, st->stream))))
+        break;
     const int sync = hip_ok(hipStreamSynchronize(st->stream));
-    pins_release(st);
     return rc ? rc : sync;
   }
   struct Piece {
@@ -1027,17 +901,12 @@ int stage_d2h_sync_impl(Staging* st, const std::vector<D2HSeg>& segs) {
   return hip_ok(hipStreamSynchronize(st->stream));
 }
 
-// ... and the caller memory the call pinned is released once nothing of the
-// call is in flight (every path above ends in a synchronised stream but an
-// early error return, which is drained here: the thread's next call reuses
-// its staging buffers).
+// ... and nothing of the call is in flight on return (every path above ends
+// in a synchronised stream but an early error return, which is drained here:
+// the thread's next call reuses its staging buffers).
 int stage_d2h_sync(Staging* st, const std::vector<D2HSeg>& segs) {
   const int rc = stage_d2h_sync_impl(st, segs);
   if (rc != LEOEC_OK) (void)hipStreamSynchronize(st->stream);
-  if (!st->pins.empty()) {
-    (void)hipStreamSynchronize(st->stream);
-    pins_release(st);
-  }
   return rc;
 }
 
@@ -1200,137 +1069,6 @@ int zc_chunked(const Plan& plan, Staging* st, const std::vector<ZcIn>& in,
   return LEOEC_OK;
 }
 
-// A per-thread call above the zero-copy cap (kGatherMax) in column chunks
-// with the link's two directions overlapped (round 5, Knobs::large_chunks).
-// The PCIe link is full duplex for DMA copies of pinned memory on separate
-// streams (97 GB/s for both directions against 57 for one), but not for
-// pageable copies, which the runtime stages through its own buffers (56 GB/s
-// for both: tools/duplex_probe.hip, profiles/r05_s28_duplex_caller_memory.log).
-// So the caller's input and output ranges are pinned in place (pin_acquire;
-// a range the runtime refuses to pin leaves the call to the one-piece copy
-// form) and chunk c of the GF(2^w) map — columns [c0, c1) of every block,
-// which depend only on the same columns of the inputs — moves as: its H2D
-// segments on the thread's input-copy stream, its launch on st->stream after
-// that copy's event, its D2H segments on the output-copy stream after the
-// launch's event, so chunk c's outputs return while chunk c + 1's inputs
-// arrive.  Device layout as the one-piece form: input i at st->buf + i *
-// stride, output o at st->buf + (nin + o) * stride.  `overlap` runs once
-// every chunk is issued.  *ran is false when the call is not split (the
-// knob, a non-GF plan, a zero-copy staging, blocks too small, no streams or
-// events, memory that cannot be pinned): the caller then takes the one-piece
-// path.  Measured and not shipped (Knobs::large_chunks = 1): registering the
-// caller's 140 MB of a 100 MiB encode per call costs more than the overlap
-// saves (2.73-3.08 ms at 4-8 chunks against 2.67-2.86 in one piece,
-// profiles/r05_s29_ref_chunks*.log).
-#ifdef LEOEC_MEASURE  // (measurement build only)
-bool take_copy_stream(Staging* st, hipStream_t* s) {
-  if (*s) return true;
-  {
-    ResourcePool& p = g_pool[st->device];
-    std::lock_guard<std::mutex> l(p.mu);
-    if (!p.streams.empty()) {
-      *s = p.streams.back();
-      p.streams.pop_back();
-      return true;
-    }
-  }
-  if (hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess) {
-    *s = nullptr;
-    return false;
-  }
-  return true;
-}
-
-int large_chunked(const Plan& plan, Staging* st, const std::vector<ZcIn>& in,
-                  const std::vector<ZcOut>& out, uint64_t bs, uint64_t stride, bool* ran,
-                  void (*overlap)(void*) = nullptr, void* arg = nullptr) {
-  *ran = false;
-  const int want = std::min(knobs().large_chunks, kStageSlots);
-  if (want <= 1 || plan.kind != Plan::kGf || st->zc || !st->buf) return LEOEC_OK;
-  const uint64_t cw = round_to((bs + (uint64_t)want - 1) / (uint64_t)want, kZcChunkAlign);
-  if (cw >= bs) return LEOEC_OK;
-  const int nc = (int)((bs + cw - 1) / cw);
-  if (!take_copy_stream(st, &st->up) || !take_copy_stream(st, &st->down)) return LEOEC_OK;
-  for (int c = 0; c < nc; ++c)
-    for (hipEvent_t* e : {&st->ev_in[c], &st->ev_k[c]})
-      if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
-        *e = nullptr;
-        return LEOEC_OK;
-      }
-  const int nin = (int)in.size(), nout = (int)out.size();
-  // pin every range (registration edges inside each: a copy never spans two)
-  std::vector<std::vector<uintptr_t>> cut_in(nin), cut_out(nout);
-  for (int i = 0; i < nin; ++i)
-    if (in[i].valid && !pin_acquire(st, in[i].host, (size_t)in[i].valid, &cut_in[i])) {
-      pins_release(st);
-      return LEOEC_OK;
-    }
-  for (int o = 0; o < nout; ++o)
-    if (out[o].n && !pin_acquire(st, out[o].host, (size_t)out[o].n, &cut_out[o])) {
-      pins_release(st);
-      return LEOEC_OK;
-    }
-  *ran = true;
-  // one copy of [h, h + n) of a pinned range, cut at its registration edges
-  auto copy = [](uint8_t* dev, uint8_t* host, size_t n, bool h2d, const std::vector<uintptr_t>& cuts,
-                 hipStream_t s) -> int {
-    const uintptr_t h = (uintptr_t)host;
-    size_t off = 0;
-    auto piece = [&](size_t stop) -> int {
-      if (stop <= off) return LEOEC_OK;
-      const hipError_t e = h2d ? hipMemcpyAsync(dev + off, host + off, stop - off, hipMemcpyHostToDevice, s)
-                               : hipMemcpyAsync(host + off, dev + off, stop - off, hipMemcpyDeviceToHost, s);
-      off = stop;
-      return hip_ok(e);
-    };
-    for (uintptr_t e : cuts)
-      if (e > h && e < h + n)
-        if (int rc = piece((size_t)(e - h))) return rc;
-    return piece(n);
-  };
-  int rc = LEOEC_OK;
-  for (int c = 0; c < nc && rc == LEOEC_OK; ++c) {
-    const uint64_t c0 = (uint64_t)c * cw, len = std::min(cw, bs - c0);
-    std::vector<Shard> si(nin), so(nout);
-    for (int i = 0; i < nin && rc == LEOEC_OK; ++i) {
-      const uint64_t v = in[i].valid > c0 ? std::min(in[i].valid - c0, len) : 0;
-      uint8_t* d = st->buf + (uint64_t)i * stride + c0;
-      if (v) rc = copy(d, const_cast<uint8_t*>(in[i].host) + c0, (size_t)v, true, cut_in[i], st->up);
-      si[i] = Shard{d, 0, v};
-    }
-    for (int o = 0; o < nout; ++o) so[o] = Shard{st->buf + (uint64_t)(nin + o) * stride + c0, 0, len};
-    if (rc == LEOEC_OK &&
-        (hipEventRecord(st->ev_in[c], st->up) != hipSuccess ||
-         hipStreamWaitEvent(st->stream, st->ev_in[c], 0) != hipSuccess))
-      rc = LEOEC_E_HIP;
-    if (rc == LEOEC_OK) rc = run_plan(plan, si, so, len, 1, st->stream);
-    if (rc == LEOEC_OK &&
-        (hipEventRecord(st->ev_k[c], st->stream) != hipSuccess ||
-         hipStreamWaitEvent(st->down, st->ev_k[c], 0) != hipSuccess))
-      rc = LEOEC_E_HIP;
-    for (int o = 0; o < nout && rc == LEOEC_OK; ++o) {
-      const uint64_t n = out[o].n > c0 ? std::min(out[o].n - c0, len) : 0;
-      if (n) rc = copy(const_cast<uint8_t*>(so[o].base), out[o].host + c0, (size_t)n, false, cut_out[o], st->down);
-    }
-  }
-  if (rc == LEOEC_OK && overlap) overlap(arg);  // the caller's host copies, while the chunks move
-  // every byte in host memory (or, after an error, nothing of the call in
-  // flight) before the pages are unpinned and the buffers reused
-  const hipError_t s1 = hipStreamSynchronize(st->up), s2 = hipStreamSynchronize(st->stream),
-                   s3 = hipStreamSynchronize(st->down);
-  pins_release(st);
-  if (rc == LEOEC_OK && (s1 != hipSuccess || s2 != hipSuccess || s3 != hipSuccess)) rc = LEOEC_E_HIP;
-  return rc;
-}
-
-#else
-int large_chunked(const Plan&, Staging*, const std::vector<ZcIn>&, const std::vector<ZcOut>&,
-                  uint64_t, uint64_t, bool* ran, void (*)(void*) = nullptr, void* = nullptr) {
-  *ran = false;  // the product's one-piece copies (Knobs::large_chunks = 1)
-  return LEOEC_OK;
-}
-#endif  // LEOEC_MEASURE
-
 // Stage the k survivor blocks, run the map into nwant device outputs (on the
 // calling thread's current device).  With `zouts` (the host destinations of
 // the outputs) a zero-copy call may run in column chunks (zc_chunked), which
@@ -1367,18 +1105,6 @@ int run_host_map(const Plan& plan, const uint8_t* const* blocks, const std::vect
       return LEOEC_OK;
     }
   }
-  if (!zc && zouts) {  // above the zero-copy cap: column chunks, both directions at once
-    std::vector<ZcIn> zi(k);
-    for (int i = 0; i < k; ++i) zi[i] = ZcIn{blocks[slot[i]], bs};
-    bool ran;
-    rc = large_chunked(plan, st, zi, *zouts, bs16, bs16, &ran, overlap, arg);
-    if (rc || ran) {
-      *st_out = st;
-      *dev_out = nullptr;
-      *stride_out = bs16;
-      return rc;
-    }
-  }
   std::vector<Shard> in(k), out(want.size());
   std::vector<H2DSeg> segs(k);
   for (int i = 0; i < k; ++i) {
@@ -1397,7 +1123,6 @@ int run_host_map(const Plan& plan, const uint8_t* const* blocks, const std::vect
     // copies already queued may still read this thread's pinned buffer:
     // drain them before the next call reuses it
     (void)hipStreamSynchronize(st->stream);
-    pins_release(st);
     st->zc = false;
     return rc;
   }
@@ -1489,16 +1214,14 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
   rc = stage_for((size_t)(k + m) * bs, &st, &zc);
   if (rc) return rc;
   uint8_t* base = zc ? st->zd : st->buf;
-  {  // column chunks: zero-copy (Knobs::zc_chunks) or, above its cap, DMA
-     // copies of pinned caller memory in both directions at once
-     // (Knobs::large_chunks)
+  if (zc) {  // zero-copy in column chunks (Knobs::zc_chunks)
     std::vector<ZcIn> zi(k);
     std::vector<ZcOut> zo(m);
     for (int j = 0; j < k; ++j)
       zi[j] = ZcIn{obj + (uint64_t)j * bs, clamp_valid(size, (uint64_t)j * bs, bs)};
     for (int i = 0; i < m; ++i) zo[i] = ZcOut{out + tail_bytes + (uint64_t)i * bs, bs};
     bool ran = false;
-    rc = zc ? zc_chunked(*plan, st, zi, zo, bs, bs, &ran) : large_chunked(*plan, st, zi, zo, bs, bs, &ran);
+    rc = zc_chunked(*plan, st, zi, zo, bs, bs, &ran);
     if (rc) st->zc = false;
     if (rc || ran) return rc;
   }
@@ -1511,7 +1234,6 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
   if (rc == LEOEC_OK) rc = run_plan(*plan, in, par, bs, 1, st->stream);
   if (rc) {
     (void)hipStreamSynchronize(st->stream);  // queued copies may still read the caller's object
-    pins_release(st);
     st->zc = false;
     return rc;
   }
@@ -1913,7 +1635,7 @@ extern "C" __attribute__((visibility("default"))) void leoec_measure_warm_state(
 }
 
 // Measurement build: out5 = {stagings handed off at thread exit, stagings
-// freed by a live thread, handed off with work in flight or pins held (0),
+// freed by a live thread, handed off with work in flight (0),
 // warm_devices threads started, warm_devices threads finished}.
 extern "C" __attribute__((visibility("default"))) void leoec_measure_reclaim_state(long* out5) {
   const leoec::ReclaimState s = leoec::reclaim_state();

@@ -125,9 +125,8 @@ WarmState warm_state(int dev);
 
 // The per-thread staging of exited threads (engine.cpp Staging::hand_off,
 // reclaim_drain): stagings handed off at thread exit, stagings freed by a
-// live thread, and handed-off stagings found with work in flight or pins
-// held (the invariant says none); and warm_devices' threads started /
-// finished.
+// live thread, and handed-off stagings found with work in flight (the
+// invariant says none); and warm_devices' threads started / finished.
 struct ReclaimState {
   long handed_off = 0;
   long drained = 0;

@@ -62,10 +62,7 @@ const Knobs* read_env() {
                       : v == "zerocopy" ? 4 : 0;
   }
   k->stage_chunk_kib = env_int("LEOEC_STAGE_CHUNK_KIB", k->stage_chunk_kib);
-  k->host_pin = env_int("LEOEC_HOST_PIN", k->host_pin);
-  k->host_pin_kib = env_int("LEOEC_HOST_PIN_KIB", k->host_pin_kib);
   k->zc_chunks = env_int("LEOEC_ZC_CHUNKS", k->zc_chunks);
-  k->large_chunks = env_int("LEOEC_LARGE_CHUNKS", k->large_chunks);
   k->host_batch = env_int("LEOEC_HOST_BATCH", k->host_batch);
   k->batch_window_us = env_int("LEOEC_BATCH_WINDOW_US", k->batch_window_us);
   k->hostq_depth = env_int("LEOEC_HOSTQ_DEPTH", k->hostq_depth);

@@ -17,19 +17,6 @@ struct Knobs {
   int host_staging = 0;      // LEOEC_HOST_STAGING: 0 auto, 1 pageable, 2 gather, 3 pinned ring,
                              //   4 zero-copy (kernels on pinned, device-mapped host memory)
   int stage_chunk_kib = 256; // LEOEC_STAGE_CHUNK_KIB: pinned-ring chunk
-  int host_pin = 0;          // LEOEC_HOST_PIN=1: a per-thread copy of >= 1 MiB from / to the
-                             //   caller's memory pins that memory in place (hipHostRegister,
-                             //   refcounted) and copies it in pieces of LEOEC_HOST_PIN_KIB
-                             //   (0: one copy per segment) instead of a pageable copy
-  int host_pin_kib = 0;
-  int large_chunks = 1;      // LEOEC_LARGE_CHUNKS (measurement form): a per-thread call above
-                             //   the zero-copy cap (16 MiB) of a GF(2^w) map runs in this many
-                             //   column chunks from caller memory pinned in place, each chunk's
-                             //   H2D / D2H on the thread's two copy streams (engine.cpp
-                             //   large_chunked).  Shipped 1 (one pageable copy each way):
-                             //   pinning 140 MB per call costs more than the duplex gains
-                             //   (100 MiB encode 2.67-2.86 ms one piece, 2.73-2.76 at 4 chunks,
-                             //   3.08 at 8: profiles/r05_s29_ref_chunks*.log)
   int zc_chunks = 2;         // LEOEC_ZC_CHUNKS: a per-thread zero-copy call of a GF(2^w) map
                              //   in this many column chunks, packing chunk c + 1 while
                              //   chunk c's launch runs and unpacking each as it completes

@@ -207,7 +207,6 @@ int main(int argc, char** argv) {
         leoec_measure_set_knob("LEOEC_HOSTQ_SPLIT_KIB", i % 2 ? "0" : "1024");
         leoec_measure_set_knob("LEOEC_HOSTQ_EAGER", (i / 2) % 2 ? "1" : "0");
         leoec_measure_set_knob("LEOEC_HOSTQ_SLOT_KIB", i % 3 == 0 ? "16384" : i % 3 == 1 ? "4096" : "512");
-        leoec_measure_set_knob("LEOEC_LARGE_CHUNKS", i % 3 == 0 ? "1" : i % 3 == 1 ? "8" : "3");
         ++i;
         std::this_thread::sleep_for(std::chrono::milliseconds(3));
       }
@@ -330,37 +329,16 @@ int main(int argc, char** argv) {
   }
 
   // phase 4: objects whose span is above the zero-copy cap (16 MiB): the
-  // per-thread copy path, with the caller's memory pinned in place
-  // (Knobs::host_pin) — 3 threads on the SAME object and blocks, so
-  // registrations are shared (the same source), refused (block ranges that
-  // share a page with a neighbour's registration: pageable copies instead)
-  // and released under each other's copies; the fake runtime aborts on an
-  // unregister with a copy in flight
+  // per-thread copy path (pageable copies, or the gather buffer for the
+  // survivors), 3 threads on the SAME object and blocks
   {
-#ifdef LEOEC_MEASURE
-    leoec_measure_set_knob("LEOEC_HOST_PIN", "1");
-    leoec_measure_set_knob("LEOEC_HOST_PIN_KIB", "512");
-#endif
     Case large{LEOEC_VANDRS, 10, 4, 8, (17u << 20) + 5};
     prepare(&large, 12);
     std::vector<std::thread> th;
     // (repair is left out: its span of k + 2 blocks stays under the cap)
     for (int t = 0; t < 3; ++t) th.emplace_back([&, t] { roundtrip(large, t, false); });
     for (auto& x : th) x.join();
-#ifdef LEOEC_MEASURE
-    leoec_measure_reset_knobs();
-    // the pinned form must have run: some ranges pinned (and, with three
-    // threads on one object's blocks, none left pinned afterwards)
-    {
-      std::lock_guard<std::mutex> l(fakehip::pinned().mu);
-      std::printf("large objects: %ld ranges pinned, %ld registrations refused, %zu still pinned\n",
-                  fakehip::pinned().n_registered, fakehip::pinned().n_refused,
-                  fakehip::pinned().registered.size());
-      if (fakehip::pinned().n_registered == 0) fail("the pinned large-object form never pinned");
-      if (!fakehip::pinned().registered.empty()) fail("caller memory left pinned after the calls");
-    }
-#endif
-    std::printf("large objects, pinned copies: %s\n", g_errs.empty() ? "ok" : "FAILED");
+    std::printf("large objects: %s\n", g_errs.empty() ? "ok" : "FAILED");
   }
 
   // phase 5: threads that come and go.  Each exiting caller thread hands its

@@ -360,6 +360,31 @@ def test_cauchy_large_launch_gfbk(gpu, le, oracle, n, size):
         assert gpu.equal(out[r], blocks[b]), b
 
 
+def test_host_above_zero_copy_cap(gpu, le, oracle):
+    """Host calls whose span passes the per-thread zero-copy cap (16 MiB) and
+    the batch cap: the per-thread copy path (one pageable copy each way, or
+    the gather buffer for k separate survivor binaries): encode / decode /
+    repair bit-exact with the oracle, twice over the same buffers, for every
+    class (ragged sizes; a 64 MiB + 5 B object)."""
+    cases = [("vandrs", 10, 4, 8, (64 << 20) + 5), ("isars", 10, 4, 8, (20 << 20) - 4095),
+             ("cauchyrs", 10, 4, 8, (17 << 20) + 77), ("vandrs", 5, 3, 32, 17 << 20),
+             ("liberation", 4, 2, 7, (17 << 20) + 1)]
+    for cls, k, m, w, size in cases:
+        data = rand_bytes(size, size + 19 * k)
+        ref = oracle.encode(cls, k, m, w, data)
+        for _ in range(2):
+            st, blocks = le.nif_encode(cls, (k, m, w), data, size)
+            assert st == "ok" and blocks == ref, (cls, k, m, w, size)
+            ids = list(range(m, k + m))[::-1]
+            st, out = le.nif_decode(cls, (k, m, w), [ref[b] for b in ids], ids, size)
+            assert st == "ok" and out == data, (cls, k, m, w, size)
+            lost = [0, k + m - 1]
+            avail = [b for b in range(k + m) if b not in lost]
+            st, rep = le.nif_repair(cls, (k, m, w), [ref[b] for b in avail], avail, lost)
+            assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size,
+                                                                  rep if st != "ok" else "")
+
+
 def test_golden_fixtures_gpu(gpu, le):
     """The committed restatement-derived fixtures, through the GPU engine."""
     import json

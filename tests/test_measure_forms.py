@@ -431,63 +431,6 @@ def test_host_zero_copy_chunks(gpu, le, oracle, chunks, measure):
         assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size)
 
 
-@pytest.mark.parametrize("chunks", ["1", "2", "3", "8"])
-def test_host_large_chunked(gpu, le, oracle, chunks, measure):
-    """Per-thread calls above the 16 MiB zero-copy cap in LEOEC_LARGE_CHUNKS
-    column chunks (engine.cpp large_chunked; 1: one pageable copy each way),
-    the caller's memory pinned in place: encode / decode / repair bit-exact
-    with the oracle, chunk edges inside and past the valid bytes, twice over
-    the same buffers; a bitmatrix class falls back to one piece."""
-    measure.setenv("LEOEC_LARGE_CHUNKS", chunks)
-    measure.setenv("LEOEC_HOST_BATCH", "0")
-    cases = [("vandrs", 10, 4, 8, (64 << 20) + 5), ("isars", 10, 4, 8, (20 << 20) - 4095),
-             ("vandrs", 5, 3, 32, 17 << 20), ("liberation", 4, 2, 7, (17 << 20) + 1)]
-    for cls, k, m, w, size in cases:
-        data = rand_bytes(size, size + 19 * k)
-        ref = oracle.encode(cls, k, m, w, data)
-        for _ in range(2):
-            st, blocks = le.nif_encode(cls, (k, m, w), data, size)
-            assert st == "ok" and blocks == ref, (cls, k, m, w, size)
-            ids = list(range(m, k + m))[::-1]
-            st, out = le.nif_decode(cls, (k, m, w), [ref[b] for b in ids], ids, size)
-            assert st == "ok" and out == data, (cls, k, m, w, size)
-            lost = [0, k + m - 1]
-            avail = [b for b in range(k + m) if b not in lost]
-            st, rep = le.nif_repair(cls, (k, m, w), [ref[b] for b in avail], avail, lost)
-            assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size,
-                                                                  rep if st != "ok" else "")
-
-
-@pytest.mark.parametrize("pin_kib", ["0", "512", "5120"])
-def test_host_pinned_large_objects(gpu, le, oracle, pin_kib, measure):
-    """The measurement build's pinned form for large per-thread copies
-    (LEOEC_HOST_PIN=1, engine.cpp copy_large / pin_acquire): the caller's
-    memory above 1 MiB per segment is pinned in place and copied in pieces
-    of LEOEC_HOST_PIN_KIB (0: whole segments), then released.  Encode /
-    decode / repair of objects whose spans pass the 16 MiB zero-copy cap,
-    bit-exact with the oracle, and every registration released afterwards
-    (a second round over the same buffers pins them again)."""
-    measure.setenv("LEOEC_HOST_PIN", "1")
-    measure.setenv("LEOEC_HOST_PIN_KIB", pin_kib)
-    measure.setenv("LEOEC_LARGE_CHUNKS", "1")  # the one-piece copies this test is about
-    cases = [("vandrs", 10, 4, 8, (64 << 20) + 5), ("cauchyrs", 10, 4, 8, (17 << 20) + 77),
-             ("isars", 10, 4, 8, 20 << 20), ("liberation", 4, 2, 7, (17 << 20) + 1)]
-    for cls, k, m, w, size in cases:
-        data = rand_bytes(size, size + 17 * k)
-        ref = oracle.encode(cls, k, m, w, data)
-        for _ in range(2):
-            st, blocks = le.nif_encode(cls, (k, m, w), data, size)
-            assert st == "ok" and blocks == ref, (cls, k, m, w, size)
-            ids = list(range(m, k + m))[::-1]
-            st, out = le.nif_decode(cls, (k, m, w), [ref[b] for b in ids], ids, size)
-            assert st == "ok" and out == data, (cls, k, m, w, size)
-            lost = [0, k + m - 1]
-            avail = [b for b in range(k + m) if b not in lost]
-            st, rep = le.nif_repair(cls, (k, m, w), [ref[b] for b in avail], avail, lost)
-            assert st == "ok" and rep == [ref[b] for b in lost], (cls, k, m, w, size,
-                                                                  rep if st != "ok" else "")
-
-
 @pytest.mark.parametrize("form", ["always-batch", "per-thread", "lanes4",
                                   "lanes4-always-batch", "fail-one", "zc-batch",
                                   "always-batch-slot-stream", "fail-one-slot-stream"])
