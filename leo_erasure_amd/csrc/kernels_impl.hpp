@@ -1001,15 +1001,24 @@ __device__ __forceinline__ void libb_dec_tile(const LibDecArgs& a, uint64_t o64,
     u32x4 acc[W];
 #pragma unroll
     for (int x = 0; x < W; ++x) acc[x] = u32x4{0u, 0u, 0u, 0u};
-    if (a.combine == 1u) {  // wave-uniform: XOR only the set bits
+    bool combined = false;
+#ifdef LEOEC_MEASURE
+    // (measurement form, LEOEC_LIB_DEC_COMBINE=1; w <= 7 only: beside the
+    // masked form it spills at w = 11 and 13, 1,600-1,900 VGPRs)
+    if constexpr (W <= 7) {
+      if (a.combine == 1u) {  // wave-uniform: XOR only the set bits
 #pragma unroll
-      for (int s = 0; s < 2 * W; ++s) {
-        const uint32_t bits = a.mbits[b][s];  // wave-uniform
+        for (int s = 0; s < 2 * W; ++s) {
+          const uint32_t bits = a.mbits[b][s];  // wave-uniform
 #pragma unroll
-        for (int x = 0; x < W; ++x)
-          if ((bits << x) & 0x80000000u) acc[x] ^= S[s];
+          for (int x = 0; x < W; ++x)
+            if ((bits << x) & 0x80000000u) acc[x] ^= S[s];
+        }
+        combined = true;
       }
-    } else {
+    }
+#endif
+    if (!combined) {
 #pragma unroll
       for (int s = 0; s < 2 * W; ++s) {
         const uint32_t bits = a.mbits[b][s];  // wave-uniform

@@ -33,5 +33,4 @@ done
 V3=";LEOEC_LIB_DEC_COMBINE=1"
 TAILN=6 step r06_s4_ab_lib427_combine 300 python tools/env_ab.py --coding liberation --k 4 --m 2 --w 7 --objects 1024 --rounds 4 --erased 0,1 --variants "$V3"
 TAILN=6 step r06_s4_ab_lib727_combine 300 python tools/env_ab.py --coding liberation --k 7 --m 2 --w 7 --objects 1024 --rounds 4 --erased 0,1 --repair 0,7 --variants "$V3"
-TAILN=6 step r06_s4_ab_lib10211_combine 300 python tools/env_ab.py --coding liberation --k 10 --m 2 --w 11 --objects 1024 --rounds 4 --erased 0,1 --variants "$V3"
 echo "session done"
