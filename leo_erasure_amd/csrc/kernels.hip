@@ -397,7 +397,6 @@ int launch(const LibDecApply& p, hipStream_t s) {
         a.mbits[b][q] = (b < nout && q < 2 * w) ? p.mbits[(size_t)b * 2 * w + q] : 0u;
     }
     a.vmin = vmin;
-    a.combine = kMeasureBuild ? (uint32_t)knobs().lib_dec_combine : 0u;
     hipLaunchKernelGGL(fn, dim3((uint32_t)(no * tiles)), dim3(lanes), 0, s, a);
     if (hipGetLastError() != hipSuccess) return LEOEC_E_HIP;
   }

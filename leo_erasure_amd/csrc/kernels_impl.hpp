@@ -730,8 +730,6 @@ struct LibDecArgs {
   uint32_t tiles;
   uint32_t vmin;          // min valid over every shard read or written
   uint32_t xmap;          // 1: xcd_obj_map
-  uint32_t combine;       // libb_dec_apply's D_E = B_CE^-1 S_C: 0 a masked XOR per (syndrome,
-                          // packet), 1 an XOR only where the bit is set (uniform branches)
 };
 
 constexpr int lib_dec_waves(int w) { return w <= 5 ? 4 : w <= 11 ? 3 : 2; }
@@ -1001,34 +999,17 @@ __device__ __forceinline__ void libb_dec_tile(const LibDecArgs& a, uint64_t o64,
     u32x4 acc[W];
 #pragma unroll
     for (int x = 0; x < W; ++x) acc[x] = u32x4{0u, 0u, 0u, 0u};
-    bool combined = false;
-#ifdef LEOEC_MEASURE
-    // (measurement form, LEOEC_LIB_DEC_COMBINE=1; w <= 7 only: beside the
-    // masked form it spills at w = 11 and 13, 1,600-1,900 VGPRs)
-    if constexpr (W <= 7) {
-      if (a.combine == 1u) {  // wave-uniform: XOR only the set bits
+    // (masked: an XOR only where a bit is set, behind uniform branches, read
+    // 1-4 % slower, profiles/r06_s4_ab_lib*_combine.log)
 #pragma unroll
-        for (int s = 0; s < 2 * W; ++s) {
-          const uint32_t bits = a.mbits[b][s];  // wave-uniform
+    for (int s = 0; s < 2 * W; ++s) {
+      const uint32_t bits = a.mbits[b][s];  // wave-uniform
+      if (bits != 0u) {
 #pragma unroll
-          for (int x = 0; x < W; ++x)
-            if ((bits << x) & 0x80000000u) acc[x] ^= S[s];
-        }
-        combined = true;
-      }
-    }
-#endif
-    if (!combined) {
+        for (int x = 0; x < W; ++x) {
+          const uint32_t m = (uint32_t)((int32_t)(bits << x) >> 31);
 #pragma unroll
-      for (int s = 0; s < 2 * W; ++s) {
-        const uint32_t bits = a.mbits[b][s];  // wave-uniform
-        if (bits != 0u) {
-#pragma unroll
-          for (int x = 0; x < W; ++x) {
-            const uint32_t m = (uint32_t)((int32_t)(bits << x) >> 31);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[x][e] ^= S[s][e] & m;
-          }
+          for (int e = 0; e < 4; ++e) acc[x][e] ^= S[s][e] & m;
         }
       }
     }

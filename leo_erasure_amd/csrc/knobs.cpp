@@ -99,7 +99,6 @@ const Knobs* read_env() {
   k->lib_buf = env_int("LEOEC_LIB_BUF", k->lib_buf);
   k->lib_dec_la = env_int("LEOEC_LIB_DEC_LA", k->lib_dec_la);
   k->lib_dec_cod = env_int("LEOEC_LIB_DEC_COD", k->lib_dec_cod);
-  k->lib_dec_combine = env_int("LEOEC_LIB_DEC_COMBINE", k->lib_dec_combine);
   k->gfbit_xmap = env_int("LEOEC_GFBIT_XMAP", k->gfbit_xmap);
   k->gfbit_lw = env_int("LEOEC_GFBIT_LW", k->gfbit_lw);
   k->gfbit_pf = env_int("LEOEC_GFBIT_PF", k->gfbit_pf);

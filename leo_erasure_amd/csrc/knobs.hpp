@@ -89,8 +89,6 @@ struct Knobs {
                              //   0 never (lib_apply / lib_dec_apply)
   int lib_dec_la = -1;       // LEOEC_LIB_DEC_LA: libb_dec_apply packet look-ahead (0: the block
                              //   form; -1: shipped, libb_dec_la(w, k))
-  int lib_dec_combine = 0;   // LEOEC_LIB_DEC_COMBINE=1: libb_dec_apply combines syndromes with an XOR
-                             //   per set bit (uniform branches) instead of a masked XOR per bit
   int lib_dec_cod = 1;       // LEOEC_LIB_DEC_COD=0: wanted coding blocks (repair of {data, P},
                              //   {Q}, ...) through the generic bitmatrix kernel, not syndromes
   // gfbit_inst.hip

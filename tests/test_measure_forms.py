@@ -91,9 +91,7 @@ def test_liberation_encode_forms(gpu, le, oracle, form, measure):
 @pytest.mark.parametrize("env", [{}, {"LEOEC_LIB_LA": "4"}, {"LEOEC_LIB_LA": "8"},
                                  {"LEOEC_LIB_WG": "256"}, {"LEOEC_LIB_WG": "256", "LEOEC_LIB_LA": "4"},
                                  {"LEOEC_LIB_DEC_WG": "64"}, {"LEOEC_LIB_DEC_LA": "4"},
-                                 {"LEOEC_LIB_DEC_LA": "8", "LEOEC_LIB_DEC_WG": "64"},
-                                 {"LEOEC_LIB_DEC_COMBINE": "1"},
-                                 {"LEOEC_LIB_DEC_COMBINE": "1", "LEOEC_LIB_DEC_LA": "0"}],
+                                 {"LEOEC_LIB_DEC_LA": "8", "LEOEC_LIB_DEC_WG": "64"}],
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()) or "shipped")
 def test_liberation_buffer_load_forms(gpu, le, oracle, env, measure):
     """libb_apply / libb_dec_apply (LEOEC_LIB_BUF=1: branch-free raw buffer

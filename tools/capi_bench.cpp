@@ -18,6 +18,7 @@
 //   tools/capi_bench <libleoec*.so> mid      [K=V,...]   callers() from 4, 8, 16, 32 threads
 //   tools/capi_bench <libleoec*.so> sizes    [K=V,...]   callers() at 16 KiB - 4 MiB
 //                                                        objects, 8 and 32 threads
+//   tools/capi_bench <libleoec*.so> many     [K=V,...]   callers() from 32 - 96 threads
 //   tools/capi_bench <libleoec*.so> trace32  [K=V,...]   callers() from 32 threads,
 //                                                        encode then decode (copy trace)
 // K=V: measurement-build knobs (leoec_measure_set_knob), applied after load.
@@ -333,6 +334,12 @@ int main(int argc, char** argv) {
   } else if (mode == "c32") {
     // 32 callers, encode then decode (the bench host leg's concurrency; A/B)
     for (bool dec : {false, true}) callers(32, dec);
+  } else if (mode == "many") {
+    // 32, 48, 64, 96 callers: whether more callers' packing overlaps the
+    // link's idle gaps (round 6: at 32 the next batch's last packs end after
+    // the previous batch's H2D, tools/copy_gaps.py)
+    for (bool dec : {false, true})
+      for (int T : {32, 48, 64, 96}) callers(T, dec);
   } else if (mode == "trace32") {
     // the bench host leg's shape for a copy trace (rocprofv3 --kernel-trace
     // --memory-copy-trace; tools/copy_gaps.py): 32 callers, encode then decode
