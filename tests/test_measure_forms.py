@@ -431,7 +431,8 @@ def test_host_zero_copy_chunks(gpu, le, oracle, chunks, measure):
 
 @pytest.mark.parametrize("form", ["always-batch", "per-thread", "lanes4",
                                   "lanes4-always-batch", "fail-one", "zc-batch",
-                                  "always-batch-slot-stream", "fail-one-slot-stream"])
+                                  "always-batch-slot-stream", "fail-one-slot-stream",
+                                  "always-batch-progressive", "fail-one-progressive"])
 def test_host_batching_mixed_callers(gpu, le, oracle, form, measure):
     """gpu_helpers.mixed_callers under the measurement build's queue
     policies: every call through the queue (always-batch) or none
@@ -443,9 +444,16 @@ def test_host_batching_mixed_callers(gpu, le, oracle, form, measure):
     decodes fail with LEOEC_E_HIP, every other call of the same batches
     succeeds bit-exact.  The queue's copies run on its two copy streams
     (shipped) except in the "-slot-stream" forms (LEOEC_HOSTQ_STREAMS=0: a
-    batch's copies and launches all on its slot's stream)."""
+    batch's copies and launches all on its slot's stream), and the
+    "-progressive" forms send a batch's inputs in runs of packed jobs
+    (LEOEC_HOSTQ_PROGRESSIVE, with complete batches handed over early)."""
     import ctypes
     fail_bs = None
+    if form.endswith("-progressive"):  # inputs in runs of packed jobs (LEOEC_HOSTQ_PROGRESSIVE)
+        measure.setenv("LEOEC_HOSTQ_PROGRESSIVE", "1")
+        measure.setenv("LEOEC_HOSTQ_PROG_KIB", "1024")
+        measure.setenv("LEOEC_HOSTQ_EAGER", "1")
+        form = form[:-len("-progressive")]
     if form.endswith("-slot-stream"):
         measure.setenv("LEOEC_HOSTQ_STREAMS", "0")
         form = form[:-len("-slot-stream")]
