@@ -91,8 +91,6 @@ struct Slot {
   std::vector<const HostJob*> jobs;
   std::vector<uint64_t> in_off, out_off;
   std::vector<int> job_rc;  // per job: its launch's status
-  std::vector<uint8_t> job_filled;  // per job: its inputs are packed (Knobs::hostq_progressive)
-  std::vector<uint8_t> job_sent;    //   and its input bytes' H2D is issued
   int lane = -1;
   int reserved = 0, filled = 0, readers = 0;
   int status = LEOEC_OK;    // the batch's copies and event: fails every job
@@ -198,7 +196,7 @@ bool same_map(const HostJob& a, const HostJob& b) {
 // recorded whatever happened, so the completer always waits for the work
 // that was enqueued before the slot can be reused.  Returns the status that
 // fails every job (the copies, the event).
-int launch_slot(Slot* s, bool inputs_sent = false) {
+int launch_slot(Slot* s) {
   Clock::time_point t = Clock::now();
   // Knobs::hostq_zc (measurement): the kernels read the pinned input arena
   // and write the pinned output arena over PCIe, no DMA copy either way
@@ -210,12 +208,11 @@ int launch_slot(Slot* s, bool inputs_sent = false) {
                      s->used_in >= ((uint64_t)knobs().hostq_split_kib << 10);
   hipStream_t cin = split ? s->up : s->stream;     // the input copy's stream
   hipStream_t cout = split ? s->down : s->stream;  // the output copy's stream
-  int rc = zc || inputs_sent
-               ? LEOEC_OK
-               : hipMemcpyAsync(s->d_in, s->h_in, s->used_in, hipMemcpyHostToDevice, cin) ==
-                         hipSuccess
-                     ? LEOEC_OK
-                     : LEOEC_E_HIP;
+  int rc = zc ? LEOEC_OK
+              : hipMemcpyAsync(s->d_in, s->h_in, s->used_in, hipMemcpyHostToDevice, cin) ==
+                        hipSuccess
+                    ? LEOEC_OK
+                    : LEOEC_E_HIP;
   if (rc == LEOEC_OK && !zc && hipEventRecord(s->ev_h2d, cin) != hipSuccess) rc = LEOEC_E_HIP;
   if (rc == LEOEC_OK && split && hipStreamWaitEvent(s->stream, s->ev_h2d, 0) != hipSuccess)
     rc = LEOEC_E_HIP;
@@ -278,54 +275,6 @@ int launch_slot(Slot* s, bool inputs_sent = false) {
   return rc;
 }
 
-// Knobs::hostq_progressive: a batch's input bytes go to the GPU in runs of
-// consecutive packed jobs while its last callers are still packing (the
-// round-6 copy trace: at 32 callers the next batch's last packs end after the
-// previous H2D, and the link waits for them).  A run is issued once it holds
-// at least hostq_prog_kib of input, or 1 MiB once the previous batch's H2D
-// has finished (the link would idle), or when it is the last.  Called with the
-// queue lock held, returns with it held and every job's input issued (on the
-// input-copy stream; the batch's H2D event follows them in launch_slot).
-// False if a copy could not be enqueued (the batch then fails as a whole).
-bool send_progressive(Slot* s, Slot* prev, std::unique_lock<std::mutex>& lk) {
-  const size_t n = s->jobs.size();
-  const uint64_t min_run = (uint64_t)knobs().hostq_prog_kib << 10;
-  bool ok = true;
-  size_t nsent = 0;
-  for (;;) {
-    const bool all = s->filled == s->reserved;
-    const bool idle = prev == nullptr || hipEventQuery(prev->ev_h2d) != hipErrorNotReady;
-    for (size_t i = 0; i < n;) {
-      if (!s->job_filled[i] || s->job_sent[i]) {
-        ++i;
-        continue;
-      }
-      size_t j = i + 1;
-      while (j < n && s->job_filled[j] && !s->job_sent[j]) ++j;
-      const uint64_t lo = s->in_off[i], hi = j < n ? s->in_off[j] : s->used_in;
-      // (an idle link takes a run of 1 MiB or more: small jobs wait for
-      // company rather than go as many small copies)
-      if (all || hi - lo >= min_run || (idle && hi - lo >= ((uint64_t)1 << 20))) {
-        for (size_t x = i; x < j; ++x) s->job_sent[x] = 1;
-        nsent += j - i;
-        lk.unlock();
-        if (hipMemcpyAsync(s->d_in + lo, s->h_in + lo, hi - lo, hipMemcpyHostToDevice, s->up) !=
-            hipSuccess)
-          ok = false;
-        lk.lock();
-      }
-      i = j;
-    }
-    if (nsent == n) return ok;
-    // re-check every 10 us (fills, and the previous H2D, which signals
-    // nothing); a sleep rather than a timed condition-variable wait, which
-    // this toolchain's ThreadSanitizer cannot follow (pthread_cond_clockwait)
-    lk.unlock();
-    std::this_thread::sleep_for(std::chrono::microseconds(10));
-    lk.lock();
-  }
-}
-
 void worker_main(Queue* q) {
   (void)hipSetDevice(q->device);
   std::unique_lock<std::mutex> lk(q->mu);
@@ -365,26 +314,14 @@ void worker_main(Queue* q) {
     }
     stat_add(6, us_since(s->opened));
     const Clock::time_point tf = Clock::now();
-    // (progressive inputs only where launch_slot splits the copies onto the
-    // input-copy stream: see its `split`)
-    const bool progressive = knobs().hostq_progressive && !knobs().hostq_zc &&
-                             knobs().hostq_streams == 1 && s->up &&
-                             s->used_in >= ((uint64_t)knobs().hostq_split_kib << 10);
-    bool sent_ok = true;
-    if (progressive) {
-      Slot* prev = q->last && q->last->state == St::kInflight ? q->last : nullptr;
-      sent_ok = send_progressive(s, prev, lk);
-    } else {
-      q->cv_worker.wait(lk, [s] { return s->filled == s->reserved; });
-    }
+    q->cv_worker.wait(lk, [s] { return s->filled == s->reserved; });
     stat_add(3, us_since(tf));
     stat_add(0, 1);
     stat_add(1, (double)s->jobs.size());
     s->state = St::kInflight;
     lk.unlock();
     const Clock::time_point tl = Clock::now();
-    int rc = launch_slot(s, progressive);
-    if (!sent_ok && rc == LEOEC_OK) rc = LEOEC_E_HIP;
+    const int rc = launch_slot(s);
     const double iu = us_since(tl);
     stat_add(4, iu);
 #ifdef LEOEC_MEASURE
@@ -661,8 +598,6 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
     f->in_off.clear();
     f->out_off.clear();
     f->job_rc.clear();
-    f->job_filled.clear();
-    f->job_sent.clear();
     f->reserved = f->filled = f->readers = 0;
     f->status = LEOEC_OK;
     f->opened = std::chrono::steady_clock::now();
@@ -675,8 +610,6 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
   s->used_out += a_out;
   s->jobs.push_back(&job);
   s->job_rc.push_back(LEOEC_OK);
-  s->job_filled.push_back(0);
-  s->job_sent.push_back(0);
   s->in_off.push_back(oi);
   s->out_off.push_back(oo);
   ++s->reserved;
@@ -707,7 +640,6 @@ int hostq_run(const HostJob& job, HostqTicket* ticket, void (*overlap)(void*), v
   // there (kernels_impl.hpp guarded tiles): nothing to zero
 
   lk.lock();
-  s->job_filled[idx] = 1;
   if (++s->filled == s->reserved) q->cv_worker.notify_one();
   lk.unlock();
   if (overlap) overlap(arg);

@@ -72,8 +72,6 @@ const Knobs* read_env() {
   k->hostq_split_kib = env_int("LEOEC_HOSTQ_SPLIT_KIB", k->hostq_split_kib);
   k->hostq_slot_kib = env_int("LEOEC_HOSTQ_SLOT_KIB", k->hostq_slot_kib);
   k->hostq_eager = env_int("LEOEC_HOSTQ_EAGER", k->hostq_eager);
-  k->hostq_progressive = env_int("LEOEC_HOSTQ_PROGRESSIVE", k->hostq_progressive);
-  k->hostq_prog_kib = env_int("LEOEC_HOSTQ_PROG_KIB", k->hostq_prog_kib);
   k->hostq_close = env_int("LEOEC_HOSTQ_CLOSE", k->hostq_close);
   k->hostq_direct = env_int("LEOEC_HOSTQ_DIRECT", k->hostq_direct);
   k->hostq_direct_map = env_int("LEOEC_HOSTQ_DIRECT_MAP", k->hostq_direct_map);

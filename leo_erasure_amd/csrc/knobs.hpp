@@ -38,9 +38,6 @@ struct Knobs {
                              //   another job of its size hands the slot to the worker at once
                              //   (0: the next caller finds it full, or the worker closes it when
                              //   the previous batch's H2D ends, Knobs::hostq_close)
-  int hostq_progressive = 0; // LEOEC_HOSTQ_PROGRESSIVE=1: a batch's input H2D in runs of packed jobs
-                             //   while its last callers still pack (hostq.cpp send_progressive)
-  int hostq_prog_kib = 4096; // LEOEC_HOSTQ_PROG_KIB: the smallest run issued while the link is busy
   int hostq_sync = 1;        // LEOEC_HOSTQ_SYNC: 1 poll events (hipEventQuery + yield),
                              //   0 hipEventSynchronize, 2 the same on blocking-sync events
   int hostq_close = 1;       // LEOEC_HOSTQ_CLOSE: 1 close a batch when the previous H2D is

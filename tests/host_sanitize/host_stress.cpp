@@ -206,8 +206,6 @@ int main(int argc, char** argv) {
         leoec_measure_set_knob("LEOEC_HOSTQ_STREAMS", (i / 7) % 2 ? "0" : "1");
         leoec_measure_set_knob("LEOEC_HOSTQ_SPLIT_KIB", i % 2 ? "0" : "1024");
         leoec_measure_set_knob("LEOEC_HOSTQ_EAGER", (i / 2) % 2 ? "1" : "0");
-        leoec_measure_set_knob("LEOEC_HOSTQ_PROGRESSIVE", (i / 3) % 2 ? "0" : "1");
-        leoec_measure_set_knob("LEOEC_HOSTQ_PROG_KIB", i % 2 ? "64" : "4096");
         leoec_measure_set_knob("LEOEC_HOSTQ_SLOT_KIB", i % 3 == 0 ? "16384" : i % 3 == 1 ? "4096" : "512");
         ++i;
         std::this_thread::sleep_for(std::chrono::milliseconds(3));

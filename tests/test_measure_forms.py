@@ -432,7 +432,7 @@ def test_host_zero_copy_chunks(gpu, le, oracle, chunks, measure):
 @pytest.mark.parametrize("form", ["always-batch", "per-thread", "lanes4",
                                   "lanes4-always-batch", "fail-one", "zc-batch",
                                   "always-batch-slot-stream", "fail-one-slot-stream",
-                                  "always-batch-progressive", "fail-one-progressive"])
+                                  "always-batch-eager", "fail-one-eager"])
 def test_host_batching_mixed_callers(gpu, le, oracle, form, measure):
     """gpu_helpers.mixed_callers under the measurement build's queue
     policies: every call through the queue (always-batch) or none
@@ -444,16 +444,14 @@ def test_host_batching_mixed_callers(gpu, le, oracle, form, measure):
     decodes fail with LEOEC_E_HIP, every other call of the same batches
     succeeds bit-exact.  The queue's copies run on its two copy streams
     (shipped) except in the "-slot-stream" forms (LEOEC_HOSTQ_STREAMS=0: a
-    batch's copies and launches all on its slot's stream), and the
-    "-progressive" forms send a batch's inputs in runs of packed jobs
-    (LEOEC_HOSTQ_PROGRESSIVE, with complete batches handed over early)."""
+    batch's copies and launches all on its slot's stream), and the "-eager"
+    forms hand a complete batch to the worker as its last job reserves
+    (LEOEC_HOSTQ_EAGER)."""
     import ctypes
     fail_bs = None
-    if form.endswith("-progressive"):  # inputs in runs of packed jobs (LEOEC_HOSTQ_PROGRESSIVE)
-        measure.setenv("LEOEC_HOSTQ_PROGRESSIVE", "1")
-        measure.setenv("LEOEC_HOSTQ_PROG_KIB", "1024")
+    if form.endswith("-eager"):  # complete batches handed over early (LEOEC_HOSTQ_EAGER)
         measure.setenv("LEOEC_HOSTQ_EAGER", "1")
-        form = form[:-len("-progressive")]
+        form = form[:-len("-eager")]
     if form.endswith("-slot-stream"):
         measure.setenv("LEOEC_HOSTQ_STREAMS", "0")
         form = form[:-len("-slot-stream")]
