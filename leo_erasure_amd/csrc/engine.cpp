@@ -556,8 +556,8 @@ struct Staging {
 
 // Invariant: a per-thread call leaves nothing of itself in flight when it
 // returns — stage_d2h_sync, zc_chunked and every error path synchronise the
-// thread's stream — so a thread's staging is idle whenever the thread can exit, and
-// its handles can be freed by any other thread.  reclaim_drain checks it
+// thread's stream — so a thread's staging is idle whenever the thread can
+// exit, and its handles can be freed by any other thread.  reclaim_drain checks it
 // (hipStreamQuery on each handed-off stream; a busy one is counted in
 // ReclaimState::busy and synchronised before reuse) and the sanitizer harness
 // asserts the count is zero (tests/host_sanitize/host_stress.cpp).
