@@ -1193,6 +1193,7 @@ int op_encode(int coding, int k, int m, int w, const uint8_t* obj, uint64_t size
   for (int i = 0; i < m; ++i) want[i] = k + i;
   std::shared_ptr<const Plan> plan;
   if ((rc = make_plan(*c, surv.data(), want.data(), m, &plan))) return rc;
+  reclaim_drain();  // exited threads' staging, also when every call is batched
   HostqTicket ticket;
   {  // concurrent calls: one batched H2D / launch / D2H (hostq.cpp)
     HostJob J;
@@ -1278,6 +1279,7 @@ int op_decode(int coding, int k, int m, int w, const uint8_t* const* blocks, con
   Staging* st = nullptr;
   uint8_t* dev = nullptr;
   uint64_t dstride = 0;
+  reclaim_drain();  // exited threads' staging, also when every call is batched
   HostqTicket ticket;
   std::unique_ptr<DeviceScope> on;  // the per-thread path's device, up to the last copy
   if (!want.empty()) {
@@ -1359,6 +1361,7 @@ int op_repair(int coding, int k, int m, int w, const uint8_t* const* blocks, con
   if (c->bitmatrix && (bs % (16ull * (uint64_t)w))) return LEOEC_E_BAD_SIZE;
   std::shared_ptr<const Plan> plan;
   if ((rc = make_plan(*c, surv.data(), want.data(), (int)want.size(), &plan))) return rc;
+  reclaim_drain();  // exited threads' staging, also when every call is batched
   HostqTicket ticket;
   {
     const uint64_t bs16 = round_to(bs, 16);

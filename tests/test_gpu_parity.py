@@ -489,10 +489,12 @@ def test_concurrent_callers(gpu, le, oracle):
 
 def test_thread_exit_releases_staging(gpu, le, oracle):
     """Caller threads that come and go (dirty schedulers, pools) give back their
-    per-thread stream, device buffer and pinned buffers (engine.cpp
-    Staging::release): 160 short-lived threads each run a decode (gather
-    staging) + encode of an 8 MiB object; device memory must not drift by
-    their buffers (~19 MB each would be ~3 GB)."""
+    per-thread stream, device buffer and pinned buffers: an exiting thread
+    hands them off without a HIP call (engine.cpp Staging::hand_off) and the
+    next call of a live thread frees them (reclaim_drain).  160 short-lived
+    threads each run a decode (gather staging) + encode of an 8 MiB object;
+    device memory must not drift by their buffers (~19 MB each would be
+    ~3 GB)."""
     import threading
 
     import torch
