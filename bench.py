@@ -344,11 +344,18 @@ class GpuBackend:
         return out
 
 
+HOST_CALLERS_LIB = os.path.join(ROOT, "tools", "libhost_callers.so")
+
+
 def host_rates(le, srcs, gpar, size, bs, device, seconds):
     """host-memory leoec_encode / leoec_decode through the C ABI from one
     thread per object of `srcs` (pageable numpy rows), back to back for
     `seconds` per op, on `device` (leoec_host_spread([device]): the threads'
-    own current device would be device 0).  Checked, outside the timed loops:
+    own current device would be device 0).  The caller threads are native
+    (tools/libhost_callers.so, built by build(): as a VM's schedulers call
+    the NIF), and the same loops from Python threads stay beside them as
+    `python_threads` (each ctypes call takes and drops the interpreter lock,
+    which costs 4-5 GiB/s at 32 threads).  Checked, outside the timed loops:
     every thread's encode parity equals `gpar` (the GPU's device parity of
     its object) and every decode (data blocks ERASED lost) returns the
     object.  No torch: bench.py runs it in the bench process and in the
@@ -418,19 +425,60 @@ def host_rates(le, srcs, gpar, size, bs, device, seconds):
             raise RuntimeError(f"host-path calls failed on threads {sorted(set(errs))[:8]}")
         return sum(counts) * size / dt / 2**30, sum(counts)
 
+    native = None
+    if os.path.exists(HOST_CALLERS_LIB):
+        native = ctypes.CDLL(HOST_CALLERS_LIB)
+        vp = ctypes.c_void_p
+        native.host_callers_run.restype = ctypes.c_long
+        native.host_callers_run.argtypes = [
+            vp, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+            ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp,
+            ctypes.c_int, ctypes.c_uint64, vp, vp]
+
+    def native_timed(op):
+        """the same loop from native threads (host_callers_run)"""
+        fn = ctypes.cast(L.leoec_encode if op == 0 else L.leoec_decode, ctypes.c_void_p)
+        src_p = (ctypes.c_void_p * n)(*[srcs[t].ctypes.data for t in range(n)])
+        out_p = (ctypes.c_void_p * n)(*[(outs if op == 0 else decs)[t].ctypes.data
+                                        for t in range(n)])
+        flat = (ctypes.c_void_p * (n * len(ids)))(*[block(t, i) for t in range(n) for i in ids])
+        counts = (ctypes.c_long * n)()
+        elapsed = ctypes.c_double()
+        bad = native.host_callers_run(fn, op, n, seconds, 2, K, M, W, src_p, out_p, size,
+                                      out_bytes, flat, idv, len(ids), bs, counts,
+                                      ctypes.byref(elapsed))
+        if bad:
+            raise RuntimeError(f"host-path calls failed: {bad} (native callers)")
+        total = sum(counts)
+        return total * size / elapsed.value / 2**30, total
+
     le._lib.host_spread([device])
     try:
         for t in range(n):
             if enc(t) != 0:
                 raise RuntimeError("leoec_encode failed")
         ptrs[:] = [(ctypes.c_void_p * len(ids))(*[block(t, i) for i in ids]) for t in range(n)]
-        enc_gibs, enc_calls = timed(enc)
-        dec_gibs, dec_calls = timed(dec)
-        enc_ok, dec_ok = check()
+        py_enc, py_enc_calls = timed(enc)
+        py_dec, py_dec_calls = timed(dec)
+        py_ok = check()
+        if native is not None:
+            enc_gibs, enc_calls = native_timed(0)
+            dec_gibs, dec_calls = native_timed(1)
+            enc_ok, dec_ok = check()
+            enc_ok, dec_ok = enc_ok and py_ok[0], dec_ok and py_ok[1]
+        else:
+            enc_gibs, enc_calls, dec_gibs, dec_calls = py_enc, py_enc_calls, py_dec, py_dec_calls
+            enc_ok, dec_ok = py_ok
     finally:
         le._lib.host_spread([])
+    kind = ("native threads (tools/libhost_callers.so), as a VM's schedulers call the NIF"
+            if native is not None else "Python threads (tools/libhost_callers.so not built)")
     return {"encode_GiBps": round(enc_gibs, 2), "decode_GiBps": round(dec_gibs, 2),
-            "callers": n, "seconds_per_op": seconds, "calls": [enc_calls, dec_calls],
+            "callers": n, "callers_kind": kind, "seconds_per_op": seconds,
+            "calls": [enc_calls, dec_calls],
+            "python_threads": {"encode_GiBps": round(py_enc, 2), "decode_GiBps": round(py_dec, 2),
+                               "calls": [py_enc_calls, py_dec_calls],
+                               "what": "the same loops from Python threads through ctypes"},
             "parity_vs_gpu": {"objects": n, "encode_equal": enc_ok, "decode_equal": dec_ok},
             "what": f"C ABI leoec_encode / leoec_decode (data blocks {ERASED} lost) of "
                     f"{size} B host objects from {n} threads, PCIe-inclusive "

@@ -224,3 +224,41 @@ def test_host_child_refuses_torch(monkeypatch):
         host_data, size, pattern_device, host_seconds = "", 1 << 20, 0, 0.1
     with pytest.raises(RuntimeError, match="without torch"):
         bench.host_child(A())
+
+
+def test_native_host_callers():
+    """tools/libhost_callers.so (bench.py's host leg, built by build()):
+    every thread calls the entry point back to back for the window, one call
+    each outside it; failures are counted.  Driven here with a ctypes
+    callback in place of leoec_encode (no GPU)."""
+    import ctypes
+    import bench
+    if not os.path.exists(bench.HOST_CALLERS_LIB):
+        pytest.skip("tools/libhost_callers.so not built")
+    lib = ctypes.CDLL(bench.HOST_CALLERS_LIB)
+    vp = ctypes.c_void_p
+    lib.host_callers_run.restype = ctypes.c_long
+    lib.host_callers_run.argtypes = [
+        vp, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+        ctypes.c_int, vp, vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp, ctypes.c_int,
+        ctypes.c_uint64, vp, vp]
+    ENC = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                           vp, ctypes.c_uint64, vp, ctypes.c_uint64)
+    seen = []
+
+    for rc in (0, 3):
+        def enc(coding, k, m, w, src, size, out, out_bytes, rc=rc):
+            seen.append((coding, k, m, w, size, out_bytes))
+            return rc
+        cb = ENC(enc)
+        n = 4
+        srcs = (vp * n)(*range(1, n + 1))
+        outs = (vp * n)(*range(11, 11 + n))
+        counts = (ctypes.c_long * n)()
+        el = ctypes.c_double()
+        bad = lib.host_callers_run(ctypes.cast(cb, vp), 0, n, 0.05, 2, 10, 4, 8, srcs, outs, 1000,
+                                   2000, None, None, 0, 0, counts, ctypes.byref(el))
+        assert el.value >= 0.05
+        assert all(c > 0 for c in counts), list(counts)
+        assert bad == (0 if rc == 0 else sum(counts) + n)  # every call fails, first calls too
+    assert seen[0] == (2, 10, 4, 8, 1000, 2000)
