@@ -360,6 +360,32 @@ def test_cauchy_large_launch_gfbk(gpu, le, oracle, n, size):
         assert gpu.equal(out[r], blocks[b]), b
 
 
+def test_cauchy_64MiB_objects_gfbk(gpu, le, oracle):
+    """configs[4]'s shape in cauchyrs(10,4,8): 64 x 64 MiB objects (+ 77 B,
+    ragged) are 6.0 GB of algorithmic bytes per launch, so encode and
+    decode take gfbk_apply with 6.7 MB blocks (820 tiles per object):
+    encode parity of the first and last objects against the oracle, decode
+    of data blocks 0-3 over poisoned blocks back to every object."""
+    k, m, w, cls = 10, 4, 8, "cauchyrs"
+    n, size = 64, (64 << 20) + 77
+    bs, _ = le.layout(cls, (k, m, w), size)
+    stride = (size + 15) // 16 * 16
+    g = gpu.Generator(device="cuda")
+    g.manual_seed(0x64CA)
+    objs = gpu.randint(0, 256, (n, stride), dtype=gpu.uint8, device="cuda", generator=g)
+    parity = gpu.full((n, m * bs), 0x5A, dtype=gpu.uint8, device="cuda")
+    le.device.encode(cls, (k, m, w), objs, size, parity)
+    gpu.cuda.synchronize()
+    for o in (0, n - 1):
+        ref = oracle.encode(cls, k, m, w, objs[o, :size].cpu().numpy().tobytes())
+        assert parity[o].cpu().numpy().tobytes() == b"".join(ref[k:]), f"object {o}"
+    ref = objs.clone()
+    objs[:, :m * bs] = 0xA5
+    le.device.decode(cls, (k, m, w), objs, size, parity, list(range(m)))
+    gpu.cuda.synchronize()
+    assert gpu.equal(objs[:, :size], ref[:, :size])
+
+
 def test_host_above_zero_copy_cap(gpu, le, oracle):
     """Host calls whose span passes the per-thread zero-copy cap (16 MiB) and
     the batch cap: the per-thread copy path (one pageable copy each way, or
