@@ -393,53 +393,6 @@ GfbFn pick_measure8(int r, bool acc) {
   return pick_r<8, 2>(r, acc);
 }
 
-// gfbk_persist (measurement form, LEOEC_GFBIT_FORM=6; round 6): gfbk_apply's
-// tiles from a fixed grid of LEOEC_GFBK_GRID workgroups (a multiple of 8),
-// each looping over the ids blockIdx.x + i * gridDim.x — the XCD a one-shot
-// launch would give that id, so xcd_obj_map keeps its meaning — instead of
-// one short-lived workgroup per tile (the one-wave form lost 2-4 % against
-// the shipped kernel at 1,024 objects, where each SIMD runs ~13 rounds of
-// one-wave workgroups: whether the rounds, not the form, cost it).
-template <int K, int LA, int WG>
-__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(1, 8)))
-gfbk_persist(const GfbkArgs a, uint32_t total) {
-  constexpr uint32_t TB = WG * 16u;
-  for (uint32_t b = blockIdx.x; b < total; b += gridDim.x) {
-    const uint32_t bid = a.xmap ? xcd_obj_map(b, total, a.tiles) : b;
-    const uint32_t obj = bid / a.tiles;
-    const uint32_t tile = bid - obj * a.tiles;
-    const uint32_t t0 = tile * TB;
-    const uint32_t off = t0 + threadIdx.x * 16u;
-    const bool full = t0 + TB <= a.ps && 7ull * a.ps + t0 + TB <= (uint64_t)a.vmin;
-    if (full) gfbk_tile<K, LA, WG, false, true>(a, obj, off, true);
-    else gfbk_tile<K, LA, WG, false, false>(a, obj, off, off < a.ps);
-  }
-}
-
-template <int LA, int WG>
-int launch_gfbk_persist_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
-                          hipStream_t s) {
-  GfbkArgs a;
-  a.ps = (uint32_t)(p.block_size / 8u);
-  a.tiles = packet_tiles(a.ps, WG, 16u);
-  a.vmin = 0xFFFFFFFFu;
-  for (int j = 0; j < kMaxK; ++j) {
-    a.in[j] = j < nk ? dev_shard(p.in[j0 + j], o0) : DevShard{nullptr, 0, 0, 0};
-    if (j < nk && a.in[j].valid < a.vmin) a.vmin = a.in[j].valid;
-  }
-  for (int i = 0; i < 4; ++i) {
-    a.out[i] = dev_shard(p.out[r0 + i], o0);
-    for (int j = 0; j < kMaxK; ++j)
-      a.coef[i][j] = j < nk ? p.coef[(size_t)(r0 + i) * p.K + j0 + j] : 0u;
-  }
-  a.xmap = (a.tiles <= kObjMapMaxTiles && knobs().gfbit_xmap != 0) ? 1u : 0u;
-  const uint32_t total = (uint32_t)(no * a.tiles);
-  uint32_t grid = (uint32_t)(knobs().gfbk_grid > 8 ? knobs().gfbk_grid : 8) / 8u * 8u;
-  if (grid > total) grid = total;
-  hipLaunchKernelGGL((gfbk_persist<10, LA, WG>), dim3(grid), dim3(WG), 0, s, a, total);
-  return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
-}
-
 // LEOEC_GFBIT_PF = blocks in flight (1..3), LEOEC_GFBIT_WG = 64 | 128 | 256,
 // LEOEC_GFBIT_WAVES = 2: at most 256 VGPRs (default: one wave per SIMD
 // allowed).  (The MASK = 1 form spills at every look-ahead: 512 VGPRs + 537
@@ -490,11 +443,6 @@ GfbFn pick_measure(const GfBitApply& p, int w, int r, bool acc, int nk, bool big
   // LEOEC_GFBIT_FORM=5: gfbk_apply where it applies (w = 8, K = 10, 4 rows,
   // no accumulation), the shipped kernel otherwise
   if (knobs().gfbit_form == 5 && w == 8 && r == 4 && !acc && nk == 10) return pick_gfbk();
-  // LEOEC_GFBIT_FORM=6: gfbk_persist (LEOEC_GFBIT_PF blocks ahead, 64 lanes)
-  if (knobs().gfbit_form == 6 && w == 8 && r == 4 && !acc && nk == 10) {
-    const int la = knobs().gfbit_pf;
-    return la <= 2 ? &launch_gfbk_persist_t<2, 64> : &launch_gfbk_persist_t<3, 64>;
-  }
   if (knobs().gfbit_form == 1) {
     // LEOEC_GFBIT_WG=128: 16-byte lanes in 128-lane workgroups, next block in flight
     if (w == 8 && knobs().gfbit_wg == 128) return pick_r2<8, 4, 1, 128>(r, acc);

@@ -107,7 +107,6 @@ struct Knobs {
   int gfbk_min_mib = -1;     // LEOEC_GFBK_MIN_MIB: launches of at least this many MiB of algorithmic
                              //   bytes take gfbk_apply (w = 8, K = 10, 4 rows; -1: the shipped
                              //   kGfbkMinBytes, gfbit_impl.hpp; a huge value: never)
-  int gfbk_grid = 1024;      // LEOEC_GFBK_GRID: gfbk_persist's workgroups (LEOEC_GFBIT_FORM=6)
   int gfbit_form = 0;        // LEOEC_GFBIT_FORM: 0 gfbit_apply (shipped), 1 gfb2_apply (buffer loads)
 };
 

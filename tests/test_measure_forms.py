@@ -253,9 +253,7 @@ def test_cauchy_compiled_bitmatrix_batches(gpu, le, oracle, measure, form):
     ("3", {"LEOEC_GFBIT_PF": "3"}), ("3", {"LEOEC_GFBIT_PF": "4"}), ("3", {"LEOEC_GFBIT_PF": "5"}),
     ("5", {}), ("5", {"LEOEC_GFBIT_PF": "2"}), ("5", {"LEOEC_GFBIT_PF": "3"}),
     ("5", {"LEOEC_GFBIT_WG": "64"}), ("5", {"LEOEC_GFBIT_WG": "64", "LEOEC_GFBIT_PF": "3"}),
-    ("5", {"LEOEC_GFBIT_WG": "256"}), ("5", {"LEOEC_GFBIT_WAVES": "2", "LEOEC_GFBIT_PF": "2"}),
-    ("6", {"LEOEC_GFBIT_PF": "3"}), ("6", {"LEOEC_GFBIT_PF": "2", "LEOEC_GFBK_GRID": "2048"}),
-    ("6", {"LEOEC_GFBIT_PF": "3", "LEOEC_GFBK_GRID": "8"})],
+    ("5", {"LEOEC_GFBIT_WG": "256"}), ("5", {"LEOEC_GFBIT_WAVES": "2", "LEOEC_GFBIT_PF": "2"})],
     ids=lambda e: e if isinstance(e, str) else (",".join(f"{k}={v}" for k, v in e.items()) or "default"))
 def test_cauchy_16B_forms_batches(gpu, le, oracle, measure, form, env):
     """cauchyrs through the 16-byte-access forms gfba_apply
