@@ -4,8 +4,6 @@
 // TU per w so the instances compile in parallel).
 #pragma once
 
-#include <utility>
-
 #include "kernels_impl.hpp"
 #include "knobs.hpp"
 
@@ -155,111 +153,7 @@ __device__ __forceinline__ void gfbk_tile(const GfbkArgs& a, uint64_t o64, uint3
   }
 }
 
-// gfbk_tile's arithmetic over blocks in pairs (PAIR = true; round 6,
-// measurement form LEOEC_GFBIT_PAIR=1): for each coefficient bit t and row i
-// the terms y_j * 2^t and y_{j+1} * 2^t of two adjacent blocks are added
-// with one 3-input XOR where both bits are set (v_xor3_b32) instead of two
-// XORs.  cauchyrs(10,4,8)'s encode matrix has 127 set coefficient bits (127
-// groups of 32 XORs per tile) and 93 groups in pairs: -27 % of the
-// accumulating XORs, the doubling chains unchanged.  A ring of LA + 2 blocks
-// (LA >= 2) keeps LA blocks in flight while a pair is consumed.
-template <class F, int... P>
-__device__ __forceinline__ void for_pairs(F&& f, std::integer_sequence<int, P...>) {
-  (f(std::integral_constant<int, 2 * P>{}), ...);
-}
-
-template <int K, int LA, int WG, bool FULL>
-__device__ __forceinline__ void gfbk_tile2(const GfbkArgs& a, uint64_t o64, uint32_t off,
-                                           bool live) {
-  constexpr int W = 8, R = 4, RS = LA + 2;
-  static_assert(K % 2 == 0 && LA >= 2, "blocks in pairs, a pair and its successors in the ring");
-  auto rs = [&](int j) { return shard_rsrc(a.in[j].base, a.in[j].stride, a.in[j].valid, o64, 16u); };
-  u32x4 ring[RS][W];
-  auto load = [&](int j, u32x4 (&y)[W]) {
-    const auto r = rs(j);
-#pragma unroll
-    for (int x = 0; x < W; ++x) y[x] = libb_load(r, off + (uint32_t)x * a.ps);
-  };
-  auto dbl = [&](u32x4 (&y)[W]) {  // y <- y * 2 (poly 0x11D: taps at bits 2, 3, 4)
-    const u32x4 top = y[W - 1];
-#pragma unroll
-    for (int r = W - 1; r >= 1; --r)
-      y[r] = ((DefaultPoly<W>::v >> r) & 1u) ? (y[r - 1] ^ top) : y[r - 1];
-    y[0] = top;
-  };
-  u32x4 acc[R][W];
-#pragma unroll
-  for (int i = 0; i < R; ++i)
-#pragma unroll
-    for (int x = 0; x < W; ++x) acc[i][x] = u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-  for (int u = 0; u < LA && u < K; ++u) load(u, ring[u]);
-  // one pair of blocks; called with j = 0, 2, .. as compile-time constants
-  // (a `for` over pairs stays rolled here and indexes the ring at run time)
-  auto pair = [&](auto jc) {
-    constexpr int j = decltype(jc)::value;
-    if (j + LA < K) load(j + LA, ring[(j + LA) % RS]);
-    if (j + LA + 1 < K) load(j + LA + 1, ring[(j + LA + 1) % RS]);
-    u32x4(&y0)[W] = ring[j % RS];
-    u32x4(&y1)[W] = ring[(j + 1) % RS];
-    if (!FULL) {
-#pragma unroll
-      for (int x = 0; x < W; ++x) {
-        y0[x] = libb_clip(y0[x], a.in[j].valid, off + (uint32_t)x * a.ps);
-        y1[x] = libb_clip(y1[x], a.in[j + 1].valid, off + (uint32_t)x * a.ps);
-      }
-    }
-    uint32_t c0[R], c1[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      c0[i] = a.coef[i][j];
-      c1[i] = a.coef[i][j + 1];
-    }
-#pragma unroll
-    for (int t = 0; t < W; ++t) {
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const bool b0 = (c0[i] >> t) & 1u, b1 = (c1[i] >> t) & 1u;
-        // three triangles (an if / else-if chain here makes the structurizer
-        // copy the accumulators between paths)
-        if (b0 && b1) {
-#pragma unroll
-          for (int x = 0; x < W; ++x)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              acc[i][x][e] = __builtin_amdgcn_bitop3_b32(acc[i][x][e], y0[x][e], y1[x][e], 0x96);
-        }
-        if (b0 && !b1) {
-#pragma unroll
-          for (int x = 0; x < W; ++x) acc[i][x] ^= y0[x];
-        }
-        if (!b0 && b1) {
-#pragma unroll
-          for (int x = 0; x < W; ++x) acc[i][x] ^= y1[x];
-        }
-      }
-      if (t + 1 < W) {
-        dbl(y0);
-        dbl(y1);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);  // the next pair's loads stay where the ring puts them
-  };
-  for_pairs(pair, std::make_integer_sequence<int, K / 2>{});
-  if (!live) return;
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    uint8_t* b = const_cast<uint8_t*>(a.out[i].base) + o64 * a.out[i].stride;
-#pragma unroll
-    for (int x = 0; x < W; ++x) {
-      const uint32_t at = off + (uint32_t)x * a.ps;
-      if (FULL) st16<true>(b + at, acc[i][x]);
-      else store_guarded(b + (uint32_t)x * a.ps, off, packet_valid(a.out[i].valid, x, a.ps), acc[i][x]);
-    }
-  }
-}
-
-template <int K, int LA, int WG, bool MASK, int WAVES, bool PAIR = false>
+template <int K, int LA, int WG, bool MASK, int WAVES>
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 gfbk_apply(const GfbkArgs a) {
   constexpr uint32_t TB = WG * 16u;
@@ -270,16 +164,11 @@ gfbk_apply(const GfbkArgs a) {
   const uint32_t off = t0 + threadIdx.x * 16u;
   // wave-uniform: the tile lies inside every packet of every input
   const bool full = t0 + TB <= a.ps && 7ull * a.ps + t0 + TB <= (uint64_t)a.vmin;
-  if constexpr (PAIR) {
-    if (full) gfbk_tile2<K, LA, WG, true>(a, obj, off, true);
-    else gfbk_tile2<K, LA, WG, false>(a, obj, off, off < a.ps);
-  } else {
-    if (full) gfbk_tile<K, LA, WG, MASK, true>(a, obj, off, true);
-    else gfbk_tile<K, LA, WG, MASK, false>(a, obj, off, off < a.ps);
-  }
+  if (full) gfbk_tile<K, LA, WG, MASK, true>(a, obj, off, true);
+  else gfbk_tile<K, LA, WG, MASK, false>(a, obj, off, off < a.ps);
 }
 
-template <int LA, int WG, bool MASK, int WAVES, bool PAIR = false>
+template <int LA, int WG, bool MASK, int WAVES>
 int launch_gfbk_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint64_t no,
                   hipStream_t s) {
   GfbkArgs a;
@@ -296,7 +185,7 @@ int launch_gfbk_t(const GfBitApply& p, int r0, int j0, int nk, uint64_t o0, uint
       a.coef[i][j] = j < nk ? p.coef[(size_t)(r0 + i) * p.K + j0 + j] : 0u;
   }
   a.xmap = (a.tiles <= kObjMapMaxTiles && knobs().gfbit_xmap != 0) ? 1u : 0u;
-  hipLaunchKernelGGL((gfbk_apply<10, LA, WG, MASK, WAVES, PAIR>), dim3((uint32_t)(no * a.tiles)),
+  hipLaunchKernelGGL((gfbk_apply<10, LA, WG, MASK, WAVES>), dim3((uint32_t)(no * a.tiles)),
                      dim3(WG), 0, s, a);
   return hipGetLastError() == hipSuccess ? LEOEC_OK : LEOEC_E_HIP;
 }

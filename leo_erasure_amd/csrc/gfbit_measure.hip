@@ -400,10 +400,6 @@ GfbFn pick_measure8(int r, bool acc) {
 GfbFn pick_gfbk() {
   const Knobs& kn = knobs();
   const int la = kn.gfbit_pf < 1 ? 1 : kn.gfbit_pf > 3 ? 3 : kn.gfbit_pf;
-  if (kn.gfbit_pair == 1)  // block pairs, 64 lanes, one wave per SIMD, LA = 2..4
-    return kn.gfbit_pf <= 2 ? &launch_gfbk_t<2, 64, false, 1, true>
-           : kn.gfbit_pf == 3 ? &launch_gfbk_t<3, 64, false, 1, true>
-                              : &launch_gfbk_t<4, 64, false, 1, true>;
   if (kn.gfbit_waves == 2) {
     if (kn.gfbit_wg == 64) return la == 1 ? &launch_gfbk_t<1, 64, false, 2> : &launch_gfbk_t<2, 64, false, 2>;
     return la == 1 ? &launch_gfbk_t<1, 128, false, 2> : &launch_gfbk_t<2, 128, false, 2>;

@@ -108,7 +108,6 @@ const Knobs* read_env() {
   k->gfbit_form = env_int("LEOEC_GFBIT_FORM", k->gfbit_form);
   k->gfbk_min_mib = env_int("LEOEC_GFBK_MIN_MIB", k->gfbk_min_mib);
   k->gfbit_waves = env_int("LEOEC_GFBIT_WAVES", k->gfbit_waves);
-  k->gfbit_pair = env_int("LEOEC_GFBIT_PAIR", k->gfbit_pair);
   k->gfbit_cbm = env_int("LEOEC_GFBIT_CBM", k->gfbit_cbm);
   k->gfs_mode = env_int("LEOEC_GFS_MODE", k->gfs_mode);
   k->gfs_pf = env_int("LEOEC_GFS_PF", k->gfs_pf);

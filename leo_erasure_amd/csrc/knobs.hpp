@@ -99,7 +99,6 @@ struct Knobs {
   int gfbit_ceil = 0;        // LEOEC_GFBIT_CEIL: traffic-ceiling kernel (not a code)
   int gfbit_lds = 0;         // LEOEC_GFBIT_LDS=1: LDS-staged inputs
   int gfbit_waves = 0;       // LEOEC_GFBIT_WAVES=4|5: register cap (waves per SIMD), w = 8
-  int gfbit_pair = 0;        // LEOEC_GFBIT_PAIR=1: gfbk_apply over block pairs (3-input XORs), LA 2..4
   int gfs_pf = 1;            // LEOEC_GFS_PF=2: two inputs in flight (w = 16/32, 4 rows)
   int gfs_mode = 0;          // LEOEC_GFS_MODE=1|2: w = 32 timing forms (not a code)
   int gfbit_cbm = 0;         // LEOEC_GFBIT_CBM: cauchyrs(10,4,8) encode with its bitmatrix compiled

@@ -253,9 +253,7 @@ def test_cauchy_compiled_bitmatrix_batches(gpu, le, oracle, measure, form):
     ("3", {"LEOEC_GFBIT_PF": "3"}), ("3", {"LEOEC_GFBIT_PF": "4"}), ("3", {"LEOEC_GFBIT_PF": "5"}),
     ("5", {}), ("5", {"LEOEC_GFBIT_PF": "2"}), ("5", {"LEOEC_GFBIT_PF": "3"}),
     ("5", {"LEOEC_GFBIT_WG": "64"}), ("5", {"LEOEC_GFBIT_WG": "64", "LEOEC_GFBIT_PF": "3"}),
-    ("5", {"LEOEC_GFBIT_WG": "256"}), ("5", {"LEOEC_GFBIT_WAVES": "2", "LEOEC_GFBIT_PF": "2"}),
-    ("5", {"LEOEC_GFBIT_PAIR": "1", "LEOEC_GFBIT_PF": "2"}), ("5", {"LEOEC_GFBIT_PAIR": "1", "LEOEC_GFBIT_PF": "3"}),
-    ("5", {"LEOEC_GFBIT_PAIR": "1", "LEOEC_GFBIT_PF": "4"})],
+    ("5", {"LEOEC_GFBIT_WG": "256"}), ("5", {"LEOEC_GFBIT_WAVES": "2", "LEOEC_GFBIT_PF": "2"})],
     ids=lambda e: e if isinstance(e, str) else (",".join(f"{k}={v}" for k, v in e.items()) or "default"))
 def test_cauchy_16B_forms_batches(gpu, le, oracle, measure, form, env):
     """cauchyrs through the 16-byte-access forms gfba_apply
@@ -263,7 +261,7 @@ def test_cauchy_16B_forms_batches(gpu, le, oracle, measure, form, env):
     read back at each packet's phase; round 4's gfbs_apply, form 4, ran here
     too before it was removed, code at cd96abc) and gfbk_apply (FORM=5: K = 10
     compiled in, 16-byte lanes, one wave per SIMD, blocks of loads in flight;
-    LEOEC_GFBIT_PAIR=1: its blocks in pairs, 3-input XORs; the other k fall back to the shipped kernel).  Object rows at every
+    the other k fall back to the shipped kernel).  Object rows at every
     16-byte phase mod 128 (row stride = k*bs + 48), sizes whose blocks are
     full, short (last block 103,936 of 104,960 B), one packet of 16 B, and
     empty (size 1,040: block 9 holds nothing); encode parity equal to the
